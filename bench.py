@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Benchmark: batched Goldfarb–Idnani QP solves on MI355X (BASELINE.json metric).
+
+One "step" = one batched solve (one launch of the gfx950 kernel through the C-ABI
+qpgpu_solve_batched) over the rank's resident batch of synthetic QPs, plus — when N > 1 — the
+RCCL gather of that step's results (x, f, status) to rank 0, run on a separate stream and
+double-buffered so it overlaps the next step's solve.  Inputs are generated on the host from
+the counter-based generator (qpgpu.make_problems) and copied to HBM before timing.
+
+Default workload = BASELINE.json's metric config: 65 536 x (n=7, p=6, m=14) per GPU (weak
+scaling: per-GPU work is fixed as N grows; C4's 1M QPs on 8 GPUs is --batch 131072 --gpus 8).
+
+Single-GPU:  python bench.py [--steps K --warmup W]
+Multi-GPU:   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "motion-generation-using-quadratic-programs_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import qpgpu  # noqa: E402
+
+METRIC = "QP solves/sec at n=7,p=6,m=14 batch=65536; achieved HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CONFIGS = {
+    # name: (kind, n, p, m, default batch per GPU, description)
+    "C1": ("general", 7, 6, 14, 65536, "C1/C4: 65536 x (n=7, p=6, m=14) general QPs per GPU"),
+    "C2": ("box", 7, 0, 14, 65536, "C2: 65536 x (n=7, p=0, m=14) joint-limit box QPs per GPU"),
+    "C3": ("general", 30, 6, 60, 65536, "C3: 65536 x (n=30, p=6, m=60) general QPs per GPU"),
+    "mgqp": ("general", 14, 10, 28, 65536, "mgqp level-0 shape: 65536 x (n=14, p=10, m=28)"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="C1", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="QPs per GPU (default: config's)")
+    ap.add_argument("--seed", type=int, default=2026)
+    ap.add_argument("--no-gather", action="store_true", help="skip the rank-0 result gather (N>1)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(pr, seconds):
+    """The oracle (CPU restatement, -O2, 1 thread) on the same resident batch, repeated until
+    `seconds` of wall time: a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    oracle.lib()
+    cap = 1000 + 100 * (pr.n + pr.p + pr.m)
+    chunk = min(pr.batch, 8192)
+    sub = pr.slice(0, chunk)
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        oracle.solve_batch(sub, max_steps=cap, threads=1)
+        done += chunk
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": done / el, "unit": "QP solves/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/qp_oracle.c (-O2, 1 thread) re-solving the first {chunk} QPs of the "
+                      f"same synthetic batch {done // chunk}x ({done} solves, {el:.1f} s)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    kind, n, p, m, bdef, desc = CONFIGS[args.config]
+    B = args.batch or bdef
+    pr = qpgpu.make_problems(kind, n, p, m, rank * B, (rank + 1) * B, seed=args.seed)
+    kname = qpgpu.kernel_name(n, p, m)
+    if not kname:
+        sys.exit(f"no gfx950 kernel covers (n, p, m) = {(n, p, m)}")
+    bufs = [qpgpu.DeviceBatch(pr, dev, with_iters=False)]
+    gather = world > 1 and not args.no_gather
+    if gather:  # second output set for double buffering against the in-flight gather
+        b2 = qpgpu.DeviceBatch.__new__(qpgpu.DeviceBatch)
+        b2.__dict__.update(bufs[0].__dict__)
+        b2.x = torch.empty_like(bufs[0].x)
+        b2.f = torch.empty_like(bufs[0].f)
+        b2.status = torch.empty_like(bufs[0].status)
+        bufs.append(b2)
+        packed = [torch.empty((B, n + 2), dtype=torch.float64, device=dev) for _ in range(2)]
+        recv = [torch.empty((B, n + 2), dtype=torch.float64, device=dev) for _ in range(world)] if rank == 0 else None
+        comm = torch.cuda.Stream(dev)
+        works = [None, None]
+    compute = torch.cuda.current_stream(dev)
+
+    def step(k, ev=None):
+        db = bufs[k % len(bufs)]
+        if gather and works[k % 2] is not None:
+            works[k % 2].wait()  # compute stream waits until that buffer's gather finished
+            works[k % 2] = None
+        if ev:
+            ev[0].record(compute)
+        db.solve(stream=compute)
+        if ev:
+            ev[1].record(compute)
+        if gather:
+            pk = packed[k % 2]
+            pk[:, :n].copy_(db.x)
+            pk[:, n].copy_(db.f)
+            pk[:, n + 1].copy_(db.status.to(torch.float64))
+            done = torch.cuda.Event()
+            done.record(compute)
+            with torch.cuda.stream(comm):
+                comm.wait_event(done)
+                works[k % 2] = dist.gather(pk, recv if rank == 0 else None, dst=0, async_op=True)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k, (starts[k], ends[k]))
+    if gather:
+        for w in works:
+            if w is not None:
+                w.wait()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    # kernel-only durations: HIP events bracketing each launch on the stream it runs on
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    if dist:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    st = bufs[0].status.cpu().numpy()
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    total = B * world * args.steps
+    value = total / elapsed
+    bpq = qpgpu.algorithmic_bytes_per_qp(n, p, m)
+    achieved = bpq * B / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    traffic_src = None
+    try:
+        tj = json.load(open(args.traffic_json))
+        key = f"{args.config}:{B}:{kname}"
+        if key in tj:
+            traffic = tj[key]["hbm_bytes_per_launch"]
+            traffic_src = tj[key].get("source")
+    except (OSError, ValueError):
+        pass
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "QP solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": desc, "kind": kind, "n": n, "p": p, "m": m, "batch_per_gpu": B,
+                   "global_batch": B * world, "kernel": kname,
+                   "parallelism": f"batch-sharded x{world}" + (", RCCL gather to rank 0 (overlapped)" if gather else "")},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel_ms": kern_ms, "algorithmic_bytes_per_qp": bpq,
+                     "traffic_source": traffic_src},
+        "status_ok_frac": float((st == qpgpu.QP_OK).mean()),
+    }
+    if world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(pr, args.cpu_seconds)
+    print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,127 @@
+/*
+ * qpgpu.h — C-ABI of the MI355X-native batched Goldfarb–Idnani QP solver.
+ *
+ * This is the drop-in boundary for the reference's one hot path,
+ *   double solve_quadprog(Matrix<double>& G, Vector<double>& g0,
+ *                         const Matrix<double>& CE, const Vector<double>& ce0,
+ *                         const Matrix<double>& CI, const Vector<double>& ci0,
+ *                         Vector<double>& x);
+ * declared at reference include/QuadProgpp/QuadProg++.hh:69-72 (body only in the prebuilt
+ * lib/QuadProgpp/libquadprog.a, linked at CMakeLists.txt:95) and called from
+ * src/mgqp.cpp:708 and src/mgqp.cpp:725.
+ *
+ * Problem (QuadProg++.hh:8-13, sign convention :35-37):
+ *     min 0.5 x^T G x + g0^T x   s.t.  CE^T x + ce0 = 0,  CI^T x + ci0 >= 0
+ *
+ * Plain pointers and sizes only; no C++ or torch types cross this boundary.
+ * The C++ ArrayHH signature above is re-exported by libquadprog_amd.so (see
+ * include/quadprog_amd/QuadProg++.hh), which calls qpgpu_solve_batched_host() for one QP.
+ *
+ * Layout ("QP-major, ArrayHH row-major"): QP b of a batch occupies a contiguous block in
+ * each array, and every matrix is row-major exactly as ArrayHH::Matrix stores it
+ * (Array.hh:910-919: v[0] = new T[n*m], v[i] = v[i-1] + m):
+ *     G  [b][i][j]  at  G  + b*n*n + i*n + j          (n x n)
+ *     g0 [b][i]     at  g0 + b*n + i                   (n)
+ *     CE [b][i][k]  at  CE + b*n*p + i*p + k           (n x p, i.e. the t(CE) mgqp passes)
+ *     ce0[b][k]     at  ce0 + b*p + k                  (p)
+ *     CI [b][i][k]  at  CI + b*n*m + i*m + k           (n x m, i.e. the t(CI) mgqp passes)
+ *     ci0[b][k]     at  ci0 + b*m + k                  (m)
+ *     x  [b][i]     at  x  + b*n + i                   (n, output)
+ *     f[b], status[b], iters[b]                        (outputs; iters may be NULL)
+ */
+#ifndef QPGPU_H
+#define QPGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QPGPU_ABI_VERSION 1
+
+/* ---- per-QP status (what the reference does for that QP) -------------------------------- */
+enum qpgpu_qp_status {
+  /* solve_quadprog returned normally; f[b] is its return value (may be NaN, as mgqp.cpp:717 expects). */
+  QPGPU_QP_OK = 0,
+  /* returned std::numeric_limits<double>::infinity() through the "t >= inf" exit
+     (QuadProg++.hh:27-29: problem infeasible, x not meaningful); f[b] = +inf. */
+  QPGPU_QP_INFEASIBLE = 1,
+  /* cholesky_decomposition hit sum <= 0: the reference prints G and throws
+     std::logic_error("Error in cholesky decomposition, sum: <sum>").  f[b] holds that sum. */
+  QPGPU_QP_NOT_POSITIVE_DEFINITE = 2,
+  /* add_constraint failed in the equality phase: std::runtime_error("Constraints are linearly
+     dependent").  f[b] holds the objective accumulated so far. */
+  QPGPU_QP_DEPENDENT = 3,
+  /* The safety cap on active-set steps was reached.  The reference has no cap (it would loop);
+     the cap only exists so every GPU wave terminates and never fires on terminating problems. */
+  QPGPU_QP_MAX_ITER = 4
+};
+
+/* ---- API return codes ------------------------------------------------------------------- */
+enum qpgpu_error {
+  QPGPU_SUCCESS = 0,
+  QPGPU_ERR_INVALID_ARGUMENT = 1,  /* NULL pointer, negative size, n == 0, ...              */
+  QPGPU_ERR_UNSUPPORTED_SHAPE = 2, /* (n, p, m) outside what the compiled kernels cover      */
+  QPGPU_ERR_HIP = 3,               /* a HIP runtime call failed (message: qpgpu_last_error) */
+  QPGPU_ERR_NO_DEVICE = 4          /* no gfx950 device visible                              */
+};
+
+/* flags */
+#define QPGPU_FLAG_WRITE_FACTOR 0x1u  /* write the Cholesky factor back into G, as the
+                                          reference does (QuadProg++.hh:42-45).  Off by default
+                                          in batched use: it is extra HBM traffic. */
+
+typedef struct qpgpu_problem_desc {
+  int32_t n;         /* variables                      (G.ncols() in the reference)  */
+  int32_t p;         /* equality constraints           (CE.ncols())                  */
+  int32_t m;         /* inequality constraints         (CI.ncols())                  */
+  int32_t max_iter;  /* safety cap on active-set steps per QP; <= 0 selects the default */
+  int64_t batch;     /* number of independent QPs                                    */
+  uint32_t flags;    /* QPGPU_FLAG_*                                                  */
+  uint32_t reserved; /* must be 0                                                     */
+} qpgpu_problem_desc;
+
+/* Solve `d->batch` independent QPs.  Every pointer is DEVICE memory (hipMalloc'd or a torch
+ * tensor's data_ptr on the current device); `stream` is a hipStream_t (NULL = default stream).
+ * The call only enqueues work: it does not synchronise and allocates nothing, so it can be
+ * captured into a hipGraph.  G is read-only unless QPGPU_FLAG_WRITE_FACTOR is set.
+ * `iters` (l1 passes per QP, the reference's `iter`) may be NULL.
+ * Replaces: the per-QP call at reference src/mgqp.cpp:708, batched. */
+int qpgpu_solve_batched(const qpgpu_problem_desc* d,
+                        double* G, const double* g0,
+                        const double* CE, const double* ce0,
+                        const double* CI, const double* ci0,
+                        double* x, double* f, int32_t* status, int32_t* iters,
+                        void* stream);
+
+/* Same, with HOST pointers: copies the inputs to the device, solves, copies the outputs back
+ * and synchronises.  This is what the ArrayHH drop-in (libquadprog_amd.so) calls for each
+ * solve_quadprog(); it always runs the HIP kernel (there is no CPU path in the product).
+ * G receives the Cholesky factor when QPGPU_FLAG_WRITE_FACTOR is set. */
+int qpgpu_solve_batched_host(const qpgpu_problem_desc* d,
+                             double* G, const double* g0,
+                             const double* CE, const double* ce0,
+                             const double* CI, const double* ci0,
+                             double* x, double* f, int32_t* status, int32_t* iters);
+
+/* Largest n / m / p the compiled kernels accept (0 if no device code). */
+int qpgpu_max_n(void);
+int qpgpu_max_m(void);
+
+/* Name of the kernel variant qpgpu_solve_batched would launch for this shape ("" if none). */
+const char* qpgpu_kernel_name(int32_t n, int32_t p, int32_t m);
+
+/* Human-readable text for the last QPGPU_ERR_HIP on this thread. */
+const char* qpgpu_last_error(void);
+
+/* Number of visible HIP devices (0 if none). */
+int qpgpu_device_count(void);
+
+int qpgpu_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QPGPU_H */

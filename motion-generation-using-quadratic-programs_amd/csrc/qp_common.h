@@ -1,0 +1,60 @@
+// qp_common.h — device helpers shared by the gfx950 QP kernels.
+//
+// Every helper reproduces one reference operation bit for bit (IEEE binary64, no contraction;
+// the library is built with -ffp-contract=off).  Reference behaviour: SURVEY.md §3.2, which
+// fixes the operation order of libquadprog.a(QuadProg++.o) (the prebuilt solver behind
+// include/QuadProgpp/QuadProg++.hh:69-72).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/qpgpu.h"
+
+namespace qpk {
+
+constexpr double kEps = 2.220446049250313080847e-16;  // std::numeric_limits<double>::epsilon()
+constexpr double kSqrt2 = 1.4142135623730951;         // sqrt(2.0), .rodata +0x1e8
+
+__device__ __forceinline__ double dinf() { return __builtin_inf(); }
+
+// distance(a, b) — the reference's overflow-safe hypot (three branches), evaluated branch-free
+// so that divergent lanes do not serialise; the selected branch computes exactly the same
+// operations as the reference's.
+__device__ __forceinline__ double qp_distance(double a, double b) {
+  const double a1 = fabs(a), b1 = fabs(b);
+  const bool gt = a1 > b1, lt = b1 > a1;
+  const double num = gt ? b1 : a1;
+  const double den = gt ? a1 : b1;
+  const double t = num / den;
+  const double h = den * sqrt(1.0 + t * t);
+  return (gt || lt) ? h : a1 * kSqrt2;
+}
+
+// Ordering point for LDS hand-offs between lanes of ONE wavefront.  A QP is always owned by
+// lanes of a single wave that are converged with each other (every control decision is a
+// function of replicated values), and a wave's LDS instructions execute in issue order, so a
+// compiler-level fence is all that is needed (no s_barrier).
+__device__ __forceinline__ void sg_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct QpArgs {
+  int n, p, m, max_steps;
+  int64_t batch;
+  uint32_t flags;
+  double* G;
+  const double* g0;
+  const double* CE;
+  const double* ce0;
+  const double* CI;
+  const double* ci0;
+  double* x;
+  double* f;
+  int32_t* status;
+  int32_t* iters;
+};
+
+}  // namespace qpk

@@ -1,0 +1,311 @@
+"""qpgpu — Python host mirror of the batched solve_quadprog() C-ABI (include/qpgpu.h).
+
+The reference interface this mirrors is the solver call at reference src/mgqp.cpp:708
+(``solve_quadprog(G, g0, t(CE), ce0, t(CI), ci0, x)``, declared at
+include/QuadProgpp/QuadProg++.hh:69-72), batched: the same argument meanings, the same sign
+convention (``CE^T x + ce0 = 0``, ``CI^T x + ci0 >= 0``), the same "G is overwritten" option,
+and the same error outcomes, reported per QP as status codes instead of exceptions
+(``solve_quadprog`` in this module re-raises them exactly like the reference for one QP).
+
+Every solve runs on the gfx950 HIP kernels in ``lib/libqpgpu.so``.  If that library is missing
+this module raises at import time; there is no CPU fallback.
+
+Also hosts the synthetic problem generator of SURVEY.md §8(d): a counter-based SplitMix64
+stream keyed by (seed, qp_index, stream, element), so any shard of a batch can be generated
+independently and identically on every rank.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(_HERE, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libqpgpu.so")
+DROPIN_PATH = os.path.join(LIB_DIR, "libquadprog_amd.so")
+
+# per-QP status codes (include/qpgpu.h)
+QP_OK = 0
+QP_INFEASIBLE = 1
+QP_NOT_POSITIVE_DEFINITE = 2
+QP_DEPENDENT = 3
+QP_MAX_ITER = 4
+STATUS_NAMES = {0: "ok", 1: "infeasible", 2: "not_positive_definite", 3: "dependent", 4: "max_iter"}
+
+# API return codes
+SUCCESS = 0
+ERR_INVALID_ARGUMENT = 1
+ERR_UNSUPPORTED_SHAPE = 2
+ERR_HIP = 3
+ERR_NO_DEVICE = 4
+
+FLAG_WRITE_FACTOR = 0x1
+
+EXPORTED_SYMBOLS = (
+    "qpgpu_solve_batched",
+    "qpgpu_solve_batched_host",
+    "qpgpu_max_n",
+    "qpgpu_max_m",
+    "qpgpu_kernel_name",
+    "qpgpu_last_error",
+    "qpgpu_device_count",
+    "qpgpu_abi_version",
+)
+
+
+class QpgpuError(RuntimeError):
+    pass
+
+
+class ProblemDesc(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int32),
+        ("p", ctypes.c_int32),
+        ("m", ctypes.c_int32),
+        ("max_iter", ctypes.c_int32),
+        ("batch", ctypes.c_int64),
+        ("flags", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+    ]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"qpgpu: {LIB_PATH} is missing; build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    vp = ctypes.c_void_p
+    lib.qpgpu_solve_batched.argtypes = [ctypes.POINTER(ProblemDesc)] + [vp] * 11
+    lib.qpgpu_solve_batched.restype = ctypes.c_int
+    lib.qpgpu_solve_batched_host.argtypes = [ctypes.POINTER(ProblemDesc)] + [vp] * 10
+    lib.qpgpu_solve_batched_host.restype = ctypes.c_int
+    lib.qpgpu_kernel_name.argtypes = [ctypes.c_int32] * 3
+    lib.qpgpu_kernel_name.restype = ctypes.c_char_p
+    lib.qpgpu_last_error.restype = ctypes.c_char_p
+    lib.qpgpu_max_n.restype = ctypes.c_int
+    lib.qpgpu_max_m.restype = ctypes.c_int
+    lib.qpgpu_device_count.restype = ctypes.c_int
+    lib.qpgpu_abi_version.restype = ctypes.c_int
+    return lib
+
+
+LIB = _load()
+
+
+def kernel_name(n: int, p: int, m: int) -> str:
+    return LIB.qpgpu_kernel_name(n, p, m).decode()
+
+
+def device_count() -> int:
+    return int(LIB.qpgpu_device_count())
+
+
+def _check(rc: int, what: str):
+    if rc != SUCCESS:
+        detail = LIB.qpgpu_last_error().decode() if rc in (ERR_HIP, ERR_NO_DEVICE) else ""
+        raise QpgpuError(f"{what} failed with code {rc} {detail}".strip())
+
+
+def _ptr(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+# ----------------------------------------------------------------------------------------------
+# problem container
+# ----------------------------------------------------------------------------------------------
+@dataclass
+class Problems:
+    """A batch of QPs in the include/qpgpu.h layout (numpy float64, QP-major, row-major)."""
+
+    n: int
+    p: int
+    m: int
+    G: np.ndarray  # (B, n, n)
+    g0: np.ndarray  # (B, n)
+    CE: np.ndarray  # (B, n, p)
+    ce0: np.ndarray  # (B, p)
+    CI: np.ndarray  # (B, n, m)
+    ci0: np.ndarray  # (B, m)
+
+    @property
+    def batch(self) -> int:
+        return int(self.G.shape[0])
+
+    def slice(self, b0: int, b1: int) -> "Problems":
+        return Problems(self.n, self.p, self.m, self.G[b0:b1].copy(), self.g0[b0:b1].copy(),
+                        self.CE[b0:b1].copy(), self.ce0[b0:b1].copy(), self.CI[b0:b1].copy(),
+                        self.ci0[b0:b1].copy())
+
+    def arrays(self):
+        return (self.G, self.g0, self.CE, self.ce0, self.CI, self.ci0)
+
+
+def algorithmic_bytes_per_qp(n: int, p: int, m: int) -> int:
+    """read G, g0, CE, ce0, CI, ci0; write x and f (status excluded)."""
+    return 8 * (n * n + n + n * p + p + n * m + m) + 8 * (n + 1)
+
+
+# ----------------------------------------------------------------------------------------------
+# host-pointer solve (numpy in, numpy out) — copies through the C-ABI's host entry point
+# ----------------------------------------------------------------------------------------------
+def solve_batched_host(pr: Problems, write_factor: bool = False, max_iter: int = 0):
+    """Solve every QP of `pr` on the GPU.  Returns (x, f, status, iters).
+
+    With write_factor=True, pr.G is overwritten with each QP's Cholesky factor, as the
+    reference overwrites G (QuadProg++.hh:42-45)."""
+    B, n, p, m = pr.batch, pr.n, pr.p, pr.m
+    arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in pr.arrays()]
+    if write_factor:
+        if not (pr.G.flags.c_contiguous and pr.G.dtype == np.float64):
+            raise ValueError("write_factor needs a C-contiguous float64 G")
+        arrs[0] = pr.G
+    x = np.zeros((B, n), dtype=np.float64)
+    f = np.zeros(B, dtype=np.float64)
+    st = np.zeros(B, dtype=np.int32)
+    it = np.zeros(B, dtype=np.int32)
+    d = ProblemDesc(n, p, m, max_iter, B, FLAG_WRITE_FACTOR if write_factor else 0, 0)
+    rc = LIB.qpgpu_solve_batched_host(ctypes.byref(d), *[_ptr(a) for a in arrs], _ptr(x), _ptr(f),
+                                      _ptr(st), _ptr(it))
+    _check(rc, "qpgpu_solve_batched_host")
+    return x, f, st, it
+
+
+# ----------------------------------------------------------------------------------------------
+# device-pointer solve (torch tensors already resident in HBM)
+# ----------------------------------------------------------------------------------------------
+class DeviceBatch:
+    """Device-resident inputs/outputs for repeated solves (torch tensors on one GPU)."""
+
+    def __init__(self, pr: Problems, device, with_iters: bool = True):
+        import torch
+
+        self.n, self.p, self.m, self.batch = pr.n, pr.p, pr.m, pr.batch
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(device)
+        self.G, self.g0, self.CE, self.ce0, self.CI, self.ci0 = (t(a) for a in pr.arrays())
+        self.x = torch.zeros((self.batch, self.n), dtype=torch.float64, device=device)
+        self.f = torch.zeros(self.batch, dtype=torch.float64, device=device)
+        self.status = torch.zeros(self.batch, dtype=torch.int32, device=device)
+        self.iters = torch.zeros(self.batch, dtype=torch.int32, device=device) if with_iters else None
+
+    def solve(self, stream=None, max_iter: int = 0, write_factor: bool = False):
+        """Enqueue one batched solve on `stream` (a torch.cuda.Stream, default current)."""
+        import torch
+
+        if stream is None:
+            stream = torch.cuda.current_stream(self.x.device)
+        d = ProblemDesc(self.n, self.p, self.m, max_iter, self.batch,
+                        FLAG_WRITE_FACTOR if write_factor else 0, 0)
+        vp = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
+        rc = LIB.qpgpu_solve_batched(ctypes.byref(d), vp(self.G), vp(self.g0), vp(self.CE),
+                                     vp(self.ce0), vp(self.CI), vp(self.ci0), vp(self.x), vp(self.f),
+                                     vp(self.status), vp(self.iters),
+                                     ctypes.c_void_p(stream.cuda_stream))
+        _check(rc, "qpgpu_solve_batched")
+
+    def results(self):
+        it = None if self.iters is None else self.iters.cpu().numpy()
+        return self.x.cpu().numpy(), self.f.cpu().numpy(), self.status.cpu().numpy(), it
+
+
+# ----------------------------------------------------------------------------------------------
+# synthetic problems, counter-based so shards regenerate identically
+# ----------------------------------------------------------------------------------------------
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def _uniform01(seed: int, idx: np.ndarray, stream: int, count: int) -> np.ndarray:
+    """(len(idx), count) uniforms in (0, 1], keyed by (seed, qp index, stream, element)."""
+    idx = idx.astype(np.uint64)[:, None]
+    k = np.arange(count, dtype=np.uint64)[None, :]
+    with np.errstate(over="ignore"):
+        key = _splitmix64(np.uint64(seed & 0xFFFFFFFFFFFFFFFF) ^ np.uint64(0x5851F42D4C957F2D * (stream + 1) & 0xFFFFFFFFFFFFFFFF))
+        c = (idx << np.uint64(24)) + k
+        bits = _splitmix64(_splitmix64(c) ^ key)
+    return ((bits >> np.uint64(11)).astype(np.float64) + 1.0) * (1.0 / 9007199254740992.0)
+
+
+def _normal(seed: int, idx: np.ndarray, stream: int, count: int) -> np.ndarray:
+    u1 = _uniform01(seed, idx, 2 * stream, count)
+    u2 = _uniform01(seed, idx, 2 * stream + 1, count)
+    return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * math.pi * u2)
+
+
+def make_problems(kind: str, n: int, p: int, m: int, b0: int, b1: int, seed: int = 2026) -> Problems:
+    """Generate QPs [b0, b1) of a synthetic batch.
+
+    kind="general" (C1, C3, C4, C5): G = M^T M + n I, g0 ~ 10 N(0,1), feasible point
+        x_f ~ 0.1 N(0,1), CE ~ N(0,1), ce0 = -CE^T x_f, CI ~ N(0,1), ci0 = -CI^T x_f + |N(0,1)|.
+    kind="box" (C2, mgqp joint-limit ordering, reference src/mgqp.cpp:1111-1112): same G, g0, CE;
+        CI = [-I, +I] (m = 2n), ci0 = [hi; -lo] with hi = -lo = 1.
+    """
+    idx = np.arange(b0, b1, dtype=np.uint64)
+    B = b1 - b0
+    M = _normal(seed, idx, 0, n * n).reshape(B, n, n)
+    G = np.einsum("bki,bkj->bij", M, M) + n * np.eye(n)[None]
+    g0 = 10.0 * _normal(seed, idx, 1, n)
+    xf = 0.1 * _normal(seed, idx, 2, n)
+    CE = _normal(seed, idx, 3, n * p).reshape(B, n, p)
+    ce0 = -np.einsum("bnp,bn->bp", CE, xf)
+    if kind == "general":
+        CI = _normal(seed, idx, 4, n * m).reshape(B, n, m)
+        ci0 = -np.einsum("bnm,bn->bm", CI, xf) + np.abs(_normal(seed, idx, 5, m))
+    elif kind == "box":
+        if m != 2 * n:
+            raise ValueError("box problems need m = 2n")
+        eye = np.eye(n)
+        CI = np.broadcast_to(np.concatenate([-eye, eye], axis=1), (B, n, m)).copy()
+        ci0 = np.ones((B, m))
+    else:
+        raise ValueError(kind)
+    return Problems(n, p, m, np.ascontiguousarray(G), np.ascontiguousarray(g0),
+                    np.ascontiguousarray(CE), np.ascontiguousarray(ce0), np.ascontiguousarray(CI),
+                    np.ascontiguousarray(ci0))
+
+
+# ----------------------------------------------------------------------------------------------
+# one QP, reference semantics (exceptions instead of status codes)
+# ----------------------------------------------------------------------------------------------
+def solve_quadprog(G: np.ndarray, g0, CE, ce0, CI, ci0):
+    """Single-QP mirror of the reference call: returns (f, x); overwrites G with its Cholesky
+    factor; raises ValueError/RuntimeError where the reference raises logic_error/runtime_error.
+    CE is n x p and CI is n x m (the t(CE) / t(CI) mgqp passes)."""
+    G = np.asarray(G)
+    n = G.shape[1]
+    CE = np.asarray(CE, dtype=np.float64).reshape(n, -1) if np.size(CE) else np.zeros((n, 0))
+    CI = np.asarray(CI, dtype=np.float64).reshape(n, -1) if np.size(CI) else np.zeros((n, 0))
+    p, m = CE.shape[1], CI.shape[1]
+    if G.shape[0] != n:
+        raise ValueError(f"The matrix G is not a squared matrix ({G.shape[0]} x {G.shape[1]})")
+    ce0 = np.asarray(ce0, dtype=np.float64).reshape(-1)
+    ci0 = np.asarray(ci0, dtype=np.float64).reshape(-1)
+    if ce0.size != p:
+        raise ValueError(f"The vector ce0 is incompatible (incorrect dimension {ce0.size}, expecting {p})")
+    if ci0.size != m:
+        raise ValueError(f"The vector ci0 is incompatible (incorrect dimension {ci0.size}, expecting {m})")
+    Gc = np.ascontiguousarray(G, dtype=np.float64).reshape(1, n, n).copy()
+    pr = Problems(n, p, m, Gc, np.asarray(g0, dtype=np.float64).reshape(1, n), CE.reshape(1, n, p),
+                  ce0.reshape(1, p), CI.reshape(1, n, m), ci0.reshape(1, m))
+    x, f, st, _ = solve_batched_host(pr, write_factor=True)
+    if G.dtype == np.float64 and G.flags.c_contiguous:
+        G[...] = Gc[0]
+    s = int(st[0])
+    if s == QP_NOT_POSITIVE_DEFINITE:
+        raise ValueError(f"Error in cholesky decomposition, sum: {f[0]:g}")
+    if s == QP_DEPENDENT:
+        raise RuntimeError("Constraints are linearly dependent")
+    if s == QP_MAX_ITER:
+        raise RuntimeError("qpgpu: active-set step cap reached")
+    return float(f[0]), x[0]

@@ -1,0 +1,119 @@
+"""GPU parity: the gfx950 kernels (through the C-ABI) against the oracle on identical inputs.
+
+Bar: per-QP status and iteration count identical, x and f BITWISE identical (the kernels keep
+the reference's operation order; north_star's stated tolerance is 1e-10 relative, and a
+failure message reports the worst relative error so a near-miss is visible)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import qp_cases
+import qpgpu
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+TOL = 1e-10  # north_star: "within 1e-10 relative"
+
+
+def _relerr(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    both_nan = np.isnan(a) & np.isnan(b)
+    same = (a == b) | both_nan
+    with np.errstate(invalid="ignore", divide="ignore"):
+        r = np.abs(a - b) / np.maximum(1.0, np.abs(b))
+    r[same] = 0.0
+    return float(np.max(r)) if r.size else 0.0
+
+
+def assert_parity(pr, label, max_iter=0, write_factor=False):
+    if not qpgpu.kernel_name(pr.n, pr.p, pr.m):
+        pytest.skip(f"no kernel for {(pr.n, pr.p, pr.m)} yet")
+    prc = qpgpu.Problems(pr.n, pr.p, pr.m, pr.G.copy(), pr.g0, pr.CE, pr.ce0, pr.CI, pr.ci0)
+    cap = max_iter if max_iter > 0 else 1000 + 100 * (pr.n + pr.p + pr.m)
+    xo, fo, so, io = oracle.solve_batch(prc, write_factor=write_factor, max_steps=cap)
+    prg = qpgpu.Problems(pr.n, pr.p, pr.m, pr.G.copy(), pr.g0, pr.CE, pr.ce0, pr.CI, pr.ci0)
+    xg, fg, sg, ig = qpgpu.solve_batched_host(prg, write_factor=write_factor, max_iter=max_iter)
+    assert np.array_equal(so, sg), f"{label}: status differs at {np.where(so != sg)[0][:10]}"
+    assert np.array_equal(io, ig), f"{label}: iteration count differs at {np.where(io != ig)[0][:10]}"
+    ok = so != qpgpu.QP_NOT_POSITIVE_DEFINITE  # x untouched on that exit (reference throws)
+    ex, ef = _relerr(xg[ok], xo[ok]), _relerr(fg, fo)
+    assert ex <= TOL and ef <= TOL, f"{label}: rel err x {ex:.3e} f {ef:.3e}"
+    bit_x = np.array_equal(xg[ok].view(np.uint64), xo[ok].view(np.uint64))
+    bit_f = np.array_equal(fg.view(np.uint64), fo.view(np.uint64))
+    assert bit_x and bit_f, f"{label}: within tolerance but not bitwise (x {ex:.3e}, f {ef:.3e})"
+    if write_factor:
+        assert np.array_equal(prg.G.view(np.uint64), prc.G.view(np.uint64)), f"{label}: factor differs"
+    return so, io
+
+
+def test_reference_kat_on_gpu(gpu):
+    kat = json.load(open(os.path.join(HERE, "golden", "reference_kat.json")))
+    for c in kat["cases"]:
+        G = np.array(c["G"])
+        f, x = qpgpu.solve_quadprog(G, c["g0"], c["CE"], c["ce0"], c["CI"], c["ci0"])
+        assert f.hex() == c["expect_f_hex"]
+        assert [v.hex() for v in x] == c["expect_x_hex"]
+        assert [[v.hex() for v in row] for row in G] == c["expect_G_after_hex"]
+
+
+@pytest.mark.parametrize("name,kind,n,p,m", qp_cases.CONFIGS)
+def test_config_parity(gpu, name, kind, n, p, m):
+    B = 4096 if n <= 16 else 512
+    assert_parity(qp_cases.make(kind, n, p, m, B), name)
+
+
+@pytest.mark.parametrize("name,pr", qp_cases.edge_cases(), ids=[c[0] for c in qp_cases.edge_cases()])
+def test_edge_parity(gpu, name, pr):
+    assert_parity(pr, name, write_factor=True)
+
+
+def test_batch_tail_and_odd_sizes(gpu):
+    for B in (1, 3, 7, 9, 63, 65, 1001):
+        assert_parity(qp_cases.make("general", 7, 6, 14, B, seed=B), f"B={B}")
+
+
+def test_max_iter_cap_matches(gpu):
+    pr = dict(qp_cases.edge_cases())["long_paths"]
+    st, _ = assert_parity(pr, "cap", max_iter=2)
+    assert (st == qpgpu.QP_MAX_ITER).any()
+
+
+def test_full_size_c1_parity(gpu):
+    """BASELINE.json metric config: 65 536 x (7, 6, 14), bitwise against the oracle."""
+    assert_parity(qpgpu.make_problems("general", 7, 6, 14, 0, 65536, seed=2026), "C1 full")
+
+
+def test_full_size_c2_parity(gpu):
+    assert_parity(qpgpu.make_problems("box", 7, 0, 14, 0, 65536, seed=2026), "C2 full")
+
+
+def test_device_api_matches_host_api(gpu):
+    import torch
+
+    pr = qpgpu.make_problems("general", 7, 6, 14, 0, 2048, seed=99)
+    db = qpgpu.DeviceBatch(pr, "cuda:0")
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        db.solve(stream=s)
+    s.synchronize()
+    x, f, st, it = db.results()
+    xh, fh, sh, ih = qpgpu.solve_batched_host(pr)
+    assert np.array_equal(x, xh) and np.array_equal(f, fh) and np.array_equal(st, sh)
+    # G untouched without the write-factor flag
+    assert np.array_equal(db.G.cpu().numpy(), pr.G)
+
+
+def test_python_mirror_raises_like_reference(gpu):
+    with pytest.raises(RuntimeError, match="Constraints are linearly dependent"):
+        qpgpu.solve_quadprog(2 * np.eye(3), np.ones(3), [[1., 1.], [2., 2.], [0., 0.]], [1., 1.],
+                             np.zeros((3, 0)), [])
+    with pytest.raises(ValueError, match=r"Error in cholesky decomposition, sum: -3"):
+        qpgpu.solve_quadprog(np.array([[1., 2.], [2., 1.]]), np.zeros(2), np.zeros((2, 0)), [],
+                             [[1.], [0.]], [0.])
+    f, x = qpgpu.solve_quadprog(np.eye(2), np.zeros(2), np.zeros((2, 0)), [],
+                                [[1., -1.], [0., 0.]], [-1., 0.])
+    assert f == float("inf")

@@ -1,0 +1,39 @@
+#!/bin/bash
+# One GPU session on the gpurun box: parity tests, smoke, bench, rocprofv3 kernel trace and
+# HBM counters.  Every GPU step has its own time limit; a crash / timeout (exit code other than
+# 0 or 1) ends the session immediately.
+#   usage: tools/gpu_session.sh TAG [steps...]   steps: pytest smoke bench prof pmc
+set -u
+TAG=${1:-session}
+shift
+STEPS=${*:-"pytest smoke bench prof pmc"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {
+  local name=$1 limit=$2
+  shift 2
+  echo "[$(date +%T)] start $name"
+  timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "stopping: $name ended with rc=$rc"
+    exit $rc
+  fi
+}
+for s in $STEPS; do
+  case $s in
+    pytest) run pytest 900 python -m pytest tests -m gpu -q -rf ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    benchall)
+      for c in C1 C2 mgqp; do run bench_$c 600 python bench.py --config $c --no-cpu; done ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c1 -- python3 bench.py --steps 20 --warmup 5 --no-cpu ;;
+    pmc)
+      run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu
+      run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu ;;
+  esac
+done
+echo "session $TAG done"
