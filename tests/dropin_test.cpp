@@ -50,7 +50,7 @@ int main() {
     }
     for (int k = 0; k < p; k++) {
       ce0[k] = 0.3 * (k + 1);
-      for (int j = 0; j < n; j++) CE[k][j] = std::sin(1.0 + k * 7 + j);
+      for (int j = 0; j < n; j++) CE[k][j] = std::sin(0.7 * (k + 1) * (j + 1) * (j + 2) + k);
     }
     for (int k = 0; k < m; k++) {  // [-I; +I] box with limits, ordering of mgqp.cpp:1111-1112
       for (int j = 0; j < n; j++) CI[k][j] = 0.0;
