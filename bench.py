@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--config", default="C1", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="QPs per GPU (default: config's)")
     ap.add_argument("--seed", type=int, default=2026)
+    ap.add_argument("--family", default=None, choices=["lane", "subgroup"],
+                    help="force a kernel family (default: the dispatcher's choice)")
+    ap.add_argument("--layout", default="tiled64", choices=["qp_major", "tiled64"],
+                    help="batch layout of the resident inputs (include/qpgpu.h)")
     ap.add_argument("--no-gather", action="store_true", help="skip the rank-0 result gather (N>1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
@@ -98,9 +102,11 @@ def main():
     B = args.batch or bdef
     pr = qpgpu.make_problems(kind, n, p, m, rank * B, (rank + 1) * B, seed=args.seed)
     kname = qpgpu.kernel_name(n, p, m)
+    if args.family:
+        kname = {"lane": f"qp_lane[n={n},m={m}]", "subgroup": f"qp_small[n={n},m={m}]"}[args.family]
     if not kname:
         sys.exit(f"no gfx950 kernel covers (n, p, m) = {(n, p, m)}")
-    bufs = [qpgpu.DeviceBatch(pr, dev, with_iters=False)]
+    bufs = [qpgpu.DeviceBatch(pr, dev, with_iters=False, layout=args.layout)]
     gather = world > 1 and not args.no_gather
     if gather:  # second output set for double buffering against the in-flight gather
         b2 = qpgpu.DeviceBatch.__new__(qpgpu.DeviceBatch)
@@ -109,8 +115,9 @@ def main():
         b2.f = torch.empty_like(bufs[0].f)
         b2.status = torch.empty_like(bufs[0].status)
         bufs.append(b2)
-        packed = [torch.empty((B, n + 2), dtype=torch.float64, device=dev) for _ in range(2)]
-        recv = [torch.empty((B, n + 2), dtype=torch.float64, device=dev) for _ in range(world)] if rank == 0 else None
+        rows = bufs[0].x.shape[0]
+        packed = [torch.empty((rows, n + 2), dtype=torch.float64, device=dev) for _ in range(2)]
+        recv = [torch.empty((rows, n + 2), dtype=torch.float64, device=dev) for _ in range(world)] if rank == 0 else None
         comm = torch.cuda.Stream(dev)
         works = [None, None]
     compute = torch.cuda.current_stream(dev)
@@ -122,14 +129,14 @@ def main():
             works[k % 2] = None
         if ev:
             ev[0].record(compute)
-        db.solve(stream=compute)
+        db.solve(stream=compute, family=args.family)
         if ev:
             ev[1].record(compute)
         if gather:
             pk = packed[k % 2]
             pk[:, :n].copy_(db.x)
-            pk[:, n].copy_(db.f)
-            pk[:, n + 1].copy_(db.status.to(torch.float64))
+            pk[:B, n].copy_(db.f)
+            pk[:B, n + 1].copy_(db.status.to(torch.float64))
             done = torch.cuda.Event()
             done.record(compute)
             with torch.cuda.stream(comm):
@@ -196,7 +203,7 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {"workload": desc, "kind": kind, "n": n, "p": p, "m": m, "batch_per_gpu": B,
-                   "global_batch": B * world, "kernel": kname,
+                   "global_batch": B * world, "kernel": kname, "layout": args.layout,
                    "parallelism": f"batch-sharded x{world}" + (", RCCL gather to rank 0 (overlapped)" if gather else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -17,9 +17,11 @@
  * The C++ ArrayHH signature above is re-exported by libquadprog_amd.so (see
  * include/quadprog_amd/QuadProg++.hh), which calls qpgpu_solve_batched_host() for one QP.
  *
- * Layout ("QP-major, ArrayHH row-major"): QP b of a batch occupies a contiguous block in
- * each array, and every matrix is row-major exactly as ArrayHH::Matrix stores it
- * (Array.hh:910-919: v[0] = new T[n*m], v[i] = v[i-1] + m):
+ * Two batch layouts (qpgpu_problem_desc.layout).  In both, a QP's matrix is row-major exactly
+ * as ArrayHH::Matrix stores it (reference Array.hh:910-919: v[0] = new T[n*m],
+ * v[i] = v[i-1] + m); e below is that row-major element index.
+ *
+ * QPGPU_LAYOUT_QP_MAJOR (0, default): QP b occupies a contiguous block in each array:
  *     G  [b][i][j]  at  G  + b*n*n + i*n + j          (n x n)
  *     g0 [b][i]     at  g0 + b*n + i                   (n)
  *     CE [b][i][k]  at  CE + b*n*p + i*p + k           (n x p, i.e. the t(CE) mgqp passes)
@@ -28,6 +30,14 @@
  *     ci0[b][k]     at  ci0 + b*m + k                  (m)
  *     x  [b][i]     at  x  + b*n + i                   (n, output)
  *     f[b], status[b], iters[b]                        (outputs; iters may be NULL)
+ *
+ * QPGPU_LAYOUT_TILED64 (1): QPs are grouped in tiles of 64; inside a tile the element index
+ * is the slow axis and the QP index the fast one, so lane t of a wavefront reading element e of
+ * QP 64k+t touches consecutive addresses (fully coalesced 512-B rows):
+ *     element e of a per-QP block of E elements (E = n*n for G, n for g0/x, n*p for CE, ...)
+ *     of QP b lives at  X + (b / 64) * 64 * E + e * 64 + (b % 64).
+ *     Arrays hold ceil(batch/64) whole tiles; f, status, iters stay one value per QP.
+ * qpgpu_relayout() converts one array between the two layouts on the device.
  */
 #ifndef QPGPU_H
 #define QPGPU_H
@@ -67,10 +77,21 @@ enum qpgpu_error {
   QPGPU_ERR_NO_DEVICE = 4          /* no gfx950 device visible                              */
 };
 
+/* batch layouts (see the top of this file) */
+#define QPGPU_LAYOUT_QP_MAJOR 0u
+#define QPGPU_LAYOUT_TILED64 1u
+
 /* flags */
 #define QPGPU_FLAG_WRITE_FACTOR 0x1u  /* write the Cholesky factor back into G, as the
                                           reference does (QuadProg++.hh:42-45).  Off by default
                                           in batched use: it is extra HBM traffic. */
+
+/* Kernel-family selection (benchmarking / testing knobs; default = fastest for the shape):
+ *   LANE      one QP per lane (qp_lane.hip, n <= 8, m <= 16)
+ *   SUBGROUP  one QP per S-lane subgroup (qp_small.hip, n <= 16, m <= 64)
+ * Forcing a family that does not cover the shape returns QPGPU_ERR_UNSUPPORTED_SHAPE. */
+#define QPGPU_FLAG_FORCE_LANE 0x100u
+#define QPGPU_FLAG_FORCE_SUBGROUP 0x200u
 
 typedef struct qpgpu_problem_desc {
   int32_t n;         /* variables                      (G.ncols() in the reference)  */
@@ -79,7 +100,7 @@ typedef struct qpgpu_problem_desc {
   int32_t max_iter;  /* safety cap on active-set steps per QP; <= 0 selects the default */
   int64_t batch;     /* number of independent QPs                                    */
   uint32_t flags;    /* QPGPU_FLAG_*                                                  */
-  uint32_t reserved; /* must be 0                                                     */
+  uint32_t layout;   /* QPGPU_LAYOUT_* (0 = QP-major)                                  */
 } qpgpu_problem_desc;
 
 /* Solve `d->batch` independent QPs.  Every pointer is DEVICE memory (hipMalloc'd or a torch
@@ -104,6 +125,13 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d,
                              const double* CE, const double* ce0,
                              const double* CI, const double* ci0,
                              double* x, double* f, int32_t* status, int32_t* iters);
+
+/* Convert one per-QP array of `elems` doubles per QP between the layouts on the device
+ * (to_tiled = 1: QP-major -> TILED64, 0: back).  src and dst must not overlap; the TILED64
+ * side holds ceil(batch/64) whole tiles (padding entries are left untouched / not read).
+ * Enqueued on `stream`, no synchronisation. */
+int qpgpu_relayout(int64_t batch, int32_t elems, const double* src, double* dst, int32_t to_tiled,
+                   void* stream);
 
 /* Largest n / m / p the compiled kernels accept (0 if no device code). */
 int qpgpu_max_n(void);

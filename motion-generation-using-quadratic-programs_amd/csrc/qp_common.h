@@ -41,8 +41,22 @@ __device__ __forceinline__ void sg_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Offset of element 0 of QP b's block of E elements; element e is at +e*T.
+// T = 1: QP-major (ArrayHH blocks back to back); T = 64: TILED64 (include/qpgpu.h).
+template <int T>
+__device__ __forceinline__ int64_t qbase(int64_t b, int E) {
+  if constexpr (T == 1)
+    return b * (int64_t)E;
+  else
+    return (b >> 6) * (int64_t)(64 * E) + (b & 63);
+}
+__device__ __forceinline__ int64_t qbase_rt(int64_t b, int E, int T) {
+  return T == 1 ? b * (int64_t)E : (b >> 6) * (int64_t)(64 * E) + (b & 63);
+}
+
 struct QpArgs {
   int n, p, m, max_steps;
+  int tile;  // 1 = QP-major, 64 = TILED64
   int64_t batch;
   uint32_t flags;
   double* G;

@@ -96,34 +96,36 @@ __global__ void __launch_bounds__(64) qp_small_kernel(const QpArgs a) {
   double* const aold = Lq + C::OFF_AOLD;
 
   const int n = a.n, p = a.p, m = a.m;
-  const int64_t nn = (int64_t)n * n;
+  const int T = a.tile;  // layout stride (include/qpgpu.h): 1 = QP-major, 64 = TILED64
   const double inf = dinf();
+  const int64_t gbase = qbase_rt(b, n * n, T);
 
   // ---------------------------------------------------------------- loads
   {
-    const double* Gb = a.G + b * nn;
+    const double* Gb = a.G + gbase;
     for (int e = ls; e < n * n; e += S) {
       const int i = e / n;
       const int j = e - i * n;
-      Pm[i * RS + j] = Gb[e];
+      Pm[i * RS + j] = Gb[(int64_t)e * T];
     }
   }
   double CIr[CPL][NM];
   double ci0r[CPL];
   {
-    const double* CIb = a.CI + b * (int64_t)n * m;
+    const double* CIb = a.CI + qbase_rt(b, n * m, T);
+    const double* ci0b = a.ci0 + qbase_rt(b, m, T);
 #pragma unroll
     for (int q = 0; q < CPL; q++) {
       const int c = ls + q * S;
       const bool own = c < m;
 #pragma unroll
-      for (int j = 0; j < NM; j++) CIr[q][j] = (own && j < n) ? CIb[j * m + c] : 0.0;
-      ci0r[q] = own ? a.ci0[b * m + c] : 0.0;
+      for (int j = 0; j < NM; j++) CIr[q][j] = (own && j < n) ? CIb[(int64_t)(j * m + c) * T] : 0.0;
+      ci0r[q] = own ? ci0b[(int64_t)c * T] : 0.0;
     }
   }
   double g0v[NM];
 #pragma unroll
-  for (int i = 0; i < NM; i++) g0v[i] = (i < n) ? a.g0[b * n + i] : 0.0;
+  for (int i = 0; i < NM; i++) g0v[i] = (i < n) ? a.g0[qbase_rt(b, n, T) + (int64_t)i * T] : 0.0;
   sg_sync();
 
   int status = QPGPU_QP_OK;
@@ -164,11 +166,11 @@ __global__ void __launch_bounds__(64) qp_small_kernel(const QpArgs a) {
     sg_sync();
   }
   if (a.flags & QPGPU_FLAG_WRITE_FACTOR) {
-    double* Gb = a.G + b * nn;
+    double* Gb = a.G + gbase;
     for (int e = ls; e < n * n; e += S) {
       const int i = e / n;
       const int j = e - i * n;
-      Gb[e] = Pm[i * RS + j];
+      Gb[(int64_t)e * T] = Pm[i * RS + j];
     }
   }
 
@@ -438,13 +440,13 @@ __global__ void __launch_bounds__(64) qp_small_kernel(const QpArgs a) {
     // ---------------------------------------------------------------- equality phase
     bool done = false;
     for (int i = 0; i < p && !done; i++) {
-      const double* CEb = a.CE + b * (int64_t)n * p;
+      const double* CEb = a.CE + qbase_rt(b, n * p, T);
 #pragma unroll
-      for (int j = 0; j < NM; j++) npv[j] = (j < n) ? CEb[j * p + i] : 0.0;
+      for (int j = 0; j < NM; j++) npv[j] = (j < n) ? CEb[(int64_t)(j * p + i) * T] : 0.0;
 #pragma unroll
       for (int q = 0; q < RPL; q++) {
         const int k = ls + q * S;
-        npo[q] = (k < n) ? CEb[k * p + i] : 0.0;
+        npo[q] = (k < n) ? CEb[(int64_t)(k * p + i) * T] : 0.0;
       }
       compute_d();
       update_z();
@@ -452,7 +454,7 @@ __global__ void __launch_bounds__(64) qp_small_kernel(const QpArgs a) {
       double t2 = 0.0;
       const double zz = dot(zv, zv);
       const double znp = dot(zv, npv);
-      if (fabs(zz) > kEps) t2 = (-dot(npv, xv) - a.ce0[b * p + i]) / znp;
+      if (fabs(zz) > kEps) t2 = (-dot(npv, xv) - a.ce0[qbase_rt(b, p, T) + (int64_t)i * T]) / znp;
 #pragma unroll
       for (int k = 0; k < NM; k++) xv[k] += t2 * zv[k];
       put<NM + 1>(uv, iq, t2);
@@ -654,7 +656,7 @@ __global__ void __launch_bounds__(64) qp_small_kernel(const QpArgs a) {
   if (write_x) {
 #pragma unroll
     for (int i = 0; i < NM; i++)
-      if (i < n && (i % S) == ls) a.x[b * n + i] = xv[i];
+      if (i < n && (i % S) == ls) a.x[qbase_rt(b, n, T) + (int64_t)i * T] = xv[i];
   }
   if (ls == 0) {
     a.f[b] = fval;

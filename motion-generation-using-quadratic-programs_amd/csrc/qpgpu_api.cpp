@@ -16,11 +16,16 @@
 extern "C" hipError_t qpk_launch_small(const qpk::QpArgs* a, hipStream_t stream, int* handled,
                                        const char** name);
 extern "C" const char* qpk_small_name(int n, int p, int m);
+extern "C" hipError_t qpk_launch_lane(const qpk::QpArgs* a, hipStream_t stream, int* handled,
+                                      const char** name);
+extern "C" const char* qpk_lane_name(int n, int p, int m);
 extern "C" hipError_t qpk_launch_medium(const qpk::QpArgs* a, hipStream_t stream, int* handled,
                                         const char** name);
 extern "C" const char* qpk_medium_name(int n, int p, int m);
 extern "C" int qpk_medium_max_n(void);
 extern "C" int qpk_medium_max_m(void);
+extern "C" hipError_t qpk_relayout(int64_t batch, int E, const double* src, double* dst,
+                                   int to_tiled, hipStream_t stream);
 
 namespace {
 
@@ -38,9 +43,13 @@ int default_max_steps(int n, int p, int m) { return 1000 + 100 * (n + p + m); }
 
 int validate(const qpgpu_problem_desc* d) {
   if (!d) return QPGPU_ERR_INVALID_ARGUMENT;
-  if (d->n <= 0 || d->p < 0 || d->m < 0 || d->batch < 0 || d->reserved != 0)
+  if (d->n <= 0 || d->p < 0 || d->m < 0 || d->batch < 0) return QPGPU_ERR_INVALID_ARGUMENT;
+  if (d->layout != QPGPU_LAYOUT_QP_MAJOR && d->layout != QPGPU_LAYOUT_TILED64)
     return QPGPU_ERR_INVALID_ARGUMENT;
-  if (d->flags & ~QPGPU_FLAG_WRITE_FACTOR) return QPGPU_ERR_INVALID_ARGUMENT;
+  const uint32_t known = QPGPU_FLAG_WRITE_FACTOR | QPGPU_FLAG_FORCE_LANE | QPGPU_FLAG_FORCE_SUBGROUP;
+  if (d->flags & ~known) return QPGPU_ERR_INVALID_ARGUMENT;
+  if ((d->flags & QPGPU_FLAG_FORCE_LANE) && (d->flags & QPGPU_FLAG_FORCE_SUBGROUP))
+    return QPGPU_ERR_INVALID_ARGUMENT;
   return QPGPU_SUCCESS;
 }
 
@@ -82,7 +91,9 @@ int qpgpu_max_m(void) {
 
 const char* qpgpu_kernel_name(int32_t n, int32_t p, int32_t m) {
   if (n <= 0 || p < 0 || m < 0) return "";
-  const char* s = qpk_small_name(n, p, m);
+  const char* s = qpk_lane_name(n, p, m);
+  if (s) return s;
+  s = qpk_small_name(n, p, m);
   if (s) return s;
   s = qpk_medium_name(n, p, m);
   return s ? s : "";
@@ -104,6 +115,7 @@ int qpgpu_solve_batched(const qpgpu_problem_desc* d, double* G, const double* g0
   a.m = d->m;
   a.max_steps = d->max_iter > 0 ? d->max_iter : default_max_steps(d->n, d->p, d->m);
   a.batch = d->batch;
+  a.tile = d->layout == QPGPU_LAYOUT_TILED64 ? 64 : 1;
   a.flags = d->flags;
   a.G = G;
   a.g0 = g0;
@@ -117,8 +129,17 @@ int qpgpu_solve_batched(const qpgpu_problem_desc* d, double* G, const double* g0
   a.iters = iters;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int handled = 0;
-  hipError_t e = qpk_launch_small(&a, s, &handled, nullptr);
-  if (!handled) e = qpk_launch_medium(&a, s, &handled, nullptr);
+  hipError_t e = hipSuccess;
+  a.flags = d->flags & QPGPU_FLAG_WRITE_FACTOR;
+  if (d->flags & QPGPU_FLAG_FORCE_LANE) {
+    e = qpk_launch_lane(&a, s, &handled, nullptr);
+  } else if (d->flags & QPGPU_FLAG_FORCE_SUBGROUP) {
+    e = qpk_launch_small(&a, s, &handled, nullptr);
+  } else {
+    e = qpk_launch_lane(&a, s, &handled, nullptr);
+    if (!handled) e = qpk_launch_small(&a, s, &handled, nullptr);
+    if (!handled) e = qpk_launch_medium(&a, s, &handled, nullptr);
+  }
   if (!handled) return QPGPU_ERR_UNSUPPORTED_SHAPE;
   if (e != hipSuccess) return hip_fail(e, "kernel launch");
   return QPGPU_SUCCESS;
@@ -140,10 +161,12 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const doubl
     return QPGPU_ERR_NO_DEVICE;
   }
   const size_t B = (size_t)d->batch, n = d->n, p = d->p, m = d->m;
+  // per-QP-block arrays hold whole tiles in the TILED64 layout
+  const size_t BB = d->layout == QPGPU_LAYOUT_TILED64 ? (B + 63) / 64 * 64 : B;
   auto al = [](size_t bytes) { return (bytes + 255) & ~(size_t)255; };
-  const size_t bG = al(B * n * n * 8), bg0 = al(B * n * 8), bCE = al(B * n * p * 8),
-               bce0 = al(B * p * 8), bCI = al(B * n * m * 8), bci0 = al(B * m * 8),
-               bx = al(B * n * 8), bf = al(B * 8), bs = al(B * 4), bi = al(B * 4);
+  const size_t bG = al(BB * n * n * 8), bg0 = al(BB * n * 8), bCE = al(BB * n * p * 8),
+               bce0 = al(BB * p * 8), bCI = al(BB * n * m * 8), bci0 = al(BB * m * 8),
+               bx = al(BB * n * 8), bf = al(B * 8), bs = al(B * 4), bi = al(B * 4);
   const size_t total = bG + bg0 + bCE + bce0 + bCI + bci0 + bx + bf + bs + bi;
   hipError_t e;
   int dev = 0;
@@ -182,25 +205,36 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const doubl
     if (!bytes) return hipSuccess;
     return hipMemcpyAsync(dst_, src, bytes, hipMemcpyHostToDevice, s);
   };
-  if ((e = h2d(dG, G, B * n * n * 8)) != hipSuccess || (e = h2d(dg0, g0, B * n * 8)) != hipSuccess ||
-      (e = h2d(dCE, CE, B * n * p * 8)) != hipSuccess ||
-      (e = h2d(dce0, ce0, B * p * 8)) != hipSuccess ||
-      (e = h2d(dCI, CI, B * n * m * 8)) != hipSuccess ||
-      (e = h2d(dci0, ci0, B * m * 8)) != hipSuccess ||
-      (e = h2d(dx, x, B * n * 8)) != hipSuccess)  // x passes through unchanged on NONPD
+  if ((e = h2d(dG, G, BB * n * n * 8)) != hipSuccess || (e = h2d(dg0, g0, BB * n * 8)) != hipSuccess ||
+      (e = h2d(dCE, CE, BB * n * p * 8)) != hipSuccess ||
+      (e = h2d(dce0, ce0, BB * p * 8)) != hipSuccess ||
+      (e = h2d(dCI, CI, BB * n * m * 8)) != hipSuccess ||
+      (e = h2d(dci0, ci0, BB * m * 8)) != hipSuccess ||
+      (e = h2d(dx, x, BB * n * 8)) != hipSuccess)  // x passes through unchanged on NONPD
     return hip_fail(e, "hipMemcpyAsync H2D");
   rc = qpgpu_solve_batched(d, dG, dg0, dCE, dce0, dCI, dci0, dx, df, dst, dit, s);
   if (rc) return rc;
   auto d2h = [&](void* dst_, const void* src, size_t bytes) -> hipError_t {
     return hipMemcpyAsync(dst_, src, bytes, hipMemcpyDeviceToHost, s);
   };
-  if ((d->flags & QPGPU_FLAG_WRITE_FACTOR) && (e = d2h(G, dG, B * n * n * 8)) != hipSuccess)
+  if ((d->flags & QPGPU_FLAG_WRITE_FACTOR) && (e = d2h(G, dG, BB * n * n * 8)) != hipSuccess)
     return hip_fail(e, "hipMemcpyAsync D2H");
-  if ((e = d2h(x, dx, B * n * 8)) != hipSuccess || (e = d2h(f, df, B * 8)) != hipSuccess ||
+  if ((e = d2h(x, dx, BB * n * 8)) != hipSuccess || (e = d2h(f, df, B * 8)) != hipSuccess ||
       (e = d2h(status, dst, B * 4)) != hipSuccess ||
       (iters && (e = d2h(iters, dit, B * 4)) != hipSuccess))
     return hip_fail(e, "hipMemcpyAsync D2H");
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  return QPGPU_SUCCESS;
+}
+
+int qpgpu_relayout(int64_t batch, int32_t elems, const double* src, double* dst, int32_t to_tiled,
+                   void* stream) {
+  if (batch < 0 || elems < 0 || (batch > 0 && elems > 0 && (!src || !dst)))
+    return QPGPU_ERR_INVALID_ARGUMENT;
+  if (batch == 0 || elems == 0) return QPGPU_SUCCESS;
+  hipError_t e = qpk_relayout(batch, elems, src, dst, to_tiled ? 1 : 0,
+                              reinterpret_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "relayout launch");
   return QPGPU_SUCCESS;
 }
 

@@ -44,6 +44,12 @@ ERR_HIP = 3
 ERR_NO_DEVICE = 4
 
 FLAG_WRITE_FACTOR = 0x1
+FLAG_FORCE_LANE = 0x100
+FLAG_FORCE_SUBGROUP = 0x200
+FAMILY_FLAGS = {None: 0, "auto": 0, "lane": FLAG_FORCE_LANE, "subgroup": FLAG_FORCE_SUBGROUP}
+LAYOUT_QP_MAJOR = 0
+LAYOUT_TILED64 = 1
+LAYOUTS = {None: 0, "qp_major": LAYOUT_QP_MAJOR, "tiled64": LAYOUT_TILED64}
 
 EXPORTED_SYMBOLS = (
     "qpgpu_solve_batched",
@@ -54,6 +60,7 @@ EXPORTED_SYMBOLS = (
     "qpgpu_last_error",
     "qpgpu_device_count",
     "qpgpu_abi_version",
+    "qpgpu_relayout",
 )
 
 
@@ -69,7 +76,7 @@ class ProblemDesc(ctypes.Structure):
         ("max_iter", ctypes.c_int32),
         ("batch", ctypes.c_int64),
         ("flags", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("layout", ctypes.c_uint32),
     ]
 
 
@@ -91,6 +98,8 @@ def _load():
     lib.qpgpu_max_m.restype = ctypes.c_int
     lib.qpgpu_device_count.restype = ctypes.c_int
     lib.qpgpu_abi_version.restype = ctypes.c_int
+    lib.qpgpu_relayout.argtypes = [ctypes.c_int64, ctypes.c_int32, vp, vp, ctypes.c_int32, vp]
+    lib.qpgpu_relayout.restype = ctypes.c_int
     return lib
 
 
@@ -145,6 +154,24 @@ class Problems:
         return (self.G, self.g0, self.CE, self.ce0, self.CI, self.ci0)
 
 
+def to_tiled64(a: np.ndarray) -> np.ndarray:
+    """(B, ...) per-QP blocks -> TILED64 flat array of ceil(B/64) tiles (include/qpgpu.h)."""
+    B = a.shape[0]
+    E = int(np.prod(a.shape[1:])) if a.ndim > 1 else 1
+    BB = (B + 63) // 64 * 64
+    pad = np.zeros((BB, E), dtype=np.float64)
+    pad[:B] = a.reshape(B, E)
+    return np.ascontiguousarray(pad.reshape(BB // 64, 64, E).transpose(0, 2, 1)).reshape(-1)
+
+
+def from_tiled64(flat: np.ndarray, B: int, shape) -> np.ndarray:
+    """Inverse of to_tiled64: returns (B, *shape)."""
+    E = int(np.prod(shape)) if len(shape) else 1
+    BB = (B + 63) // 64 * 64
+    t = np.asarray(flat).reshape(BB // 64, E, 64).transpose(0, 2, 1).reshape(BB, E)
+    return np.ascontiguousarray(t[:B]).reshape((B,) + tuple(shape))
+
+
 def algorithmic_bytes_per_qp(n: int, p: int, m: int) -> int:
     """read G, g0, CE, ce0, CI, ci0; write x and f (status excluded)."""
     return 8 * (n * n + n + n * p + p + n * m + m) + 8 * (n + 1)
@@ -153,12 +180,28 @@ def algorithmic_bytes_per_qp(n: int, p: int, m: int) -> int:
 # ----------------------------------------------------------------------------------------------
 # host-pointer solve (numpy in, numpy out) — copies through the C-ABI's host entry point
 # ----------------------------------------------------------------------------------------------
-def solve_batched_host(pr: Problems, write_factor: bool = False, max_iter: int = 0):
+def solve_batched_host(pr: Problems, write_factor: bool = False, max_iter: int = 0, family=None,
+                       layout=None):
     """Solve every QP of `pr` on the GPU.  Returns (x, f, status, iters).
 
     With write_factor=True, pr.G is overwritten with each QP's Cholesky factor, as the
-    reference overwrites G (QuadProg++.hh:42-45)."""
+    reference overwrites G (QuadProg++.hh:42-45).  layout="tiled64" sends the batch in the
+    TILED64 layout (converted here on the host) and converts x / G back."""
     B, n, p, m = pr.batch, pr.n, pr.p, pr.m
+    if LAYOUTS[layout] == LAYOUT_TILED64:
+        arrs = [to_tiled64(np.asarray(a, dtype=np.float64)) for a in pr.arrays()]
+        xt = np.zeros((B + 63) // 64 * 64 * n, dtype=np.float64)
+        f = np.zeros(B, dtype=np.float64)
+        st = np.zeros(B, dtype=np.int32)
+        it = np.zeros(B, dtype=np.int32)
+        d = ProblemDesc(n, p, m, max_iter, B,
+                        (FLAG_WRITE_FACTOR if write_factor else 0) | FAMILY_FLAGS[family], LAYOUT_TILED64)
+        rc = LIB.qpgpu_solve_batched_host(ctypes.byref(d), *[_ptr(a) for a in arrs], _ptr(xt), _ptr(f),
+                                          _ptr(st), _ptr(it))
+        _check(rc, "qpgpu_solve_batched_host")
+        if write_factor:
+            pr.G[...] = from_tiled64(arrs[0], B, (n, n))
+        return from_tiled64(xt, B, (n,)), f, st, it
     arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in pr.arrays()]
     if write_factor:
         if not (pr.G.flags.c_contiguous and pr.G.dtype == np.float64):
@@ -168,7 +211,7 @@ def solve_batched_host(pr: Problems, write_factor: bool = False, max_iter: int =
     f = np.zeros(B, dtype=np.float64)
     st = np.zeros(B, dtype=np.int32)
     it = np.zeros(B, dtype=np.int32)
-    d = ProblemDesc(n, p, m, max_iter, B, FLAG_WRITE_FACTOR if write_factor else 0, 0)
+    d = ProblemDesc(n, p, m, max_iter, B, (FLAG_WRITE_FACTOR if write_factor else 0) | FAMILY_FLAGS[family], 0)
     rc = LIB.qpgpu_solve_batched_host(ctypes.byref(d), *[_ptr(a) for a in arrs], _ptr(x), _ptr(f),
                                       _ptr(st), _ptr(it))
     _check(rc, "qpgpu_solve_batched_host")
@@ -181,25 +224,28 @@ def solve_batched_host(pr: Problems, write_factor: bool = False, max_iter: int =
 class DeviceBatch:
     """Device-resident inputs/outputs for repeated solves (torch tensors on one GPU)."""
 
-    def __init__(self, pr: Problems, device, with_iters: bool = True):
+    def __init__(self, pr: Problems, device, with_iters: bool = True, layout=None):
         import torch
 
         self.n, self.p, self.m, self.batch = pr.n, pr.p, pr.m, pr.batch
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(device)
+        self.layout = LAYOUTS[layout]
+        conv = to_tiled64 if self.layout == LAYOUT_TILED64 else (lambda a: a)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(conv(np.asarray(a, dtype=np.float64)))).to(device)
         self.G, self.g0, self.CE, self.ce0, self.CI, self.ci0 = (t(a) for a in pr.arrays())
-        self.x = torch.zeros((self.batch, self.n), dtype=torch.float64, device=device)
+        rows = (self.batch + 63) // 64 * 64 if self.layout == LAYOUT_TILED64 else self.batch
+        self.x = torch.zeros((rows, self.n), dtype=torch.float64, device=device)
         self.f = torch.zeros(self.batch, dtype=torch.float64, device=device)
         self.status = torch.zeros(self.batch, dtype=torch.int32, device=device)
         self.iters = torch.zeros(self.batch, dtype=torch.int32, device=device) if with_iters else None
 
-    def solve(self, stream=None, max_iter: int = 0, write_factor: bool = False):
+    def solve(self, stream=None, max_iter: int = 0, write_factor: bool = False, family=None):
         """Enqueue one batched solve on `stream` (a torch.cuda.Stream, default current)."""
         import torch
 
         if stream is None:
             stream = torch.cuda.current_stream(self.x.device)
         d = ProblemDesc(self.n, self.p, self.m, max_iter, self.batch,
-                        FLAG_WRITE_FACTOR if write_factor else 0, 0)
+                        (FLAG_WRITE_FACTOR if write_factor else 0) | FAMILY_FLAGS[family], self.layout)
         vp = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
         rc = LIB.qpgpu_solve_batched(ctypes.byref(d), vp(self.G), vp(self.g0), vp(self.CE),
                                      vp(self.ce0), vp(self.CI), vp(self.ci0), vp(self.x), vp(self.f),
@@ -209,7 +255,21 @@ class DeviceBatch:
 
     def results(self):
         it = None if self.iters is None else self.iters.cpu().numpy()
-        return self.x.cpu().numpy(), self.f.cpu().numpy(), self.status.cpu().numpy(), it
+        x = self.x.cpu().numpy()
+        if self.layout == LAYOUT_TILED64:
+            x = from_tiled64(x.reshape(-1), self.batch, (self.n,))
+        return x, self.f.cpu().numpy(), self.status.cpu().numpy(), it
+
+
+def relayout(src, dst, batch: int, elems: int, to_tiled: bool, stream=None):
+    """Device conversion of one per-QP array between layouts (torch tensors)."""
+    import torch
+
+    if stream is None:
+        stream = torch.cuda.current_stream(src.device)
+    rc = LIB.qpgpu_relayout(batch, elems, ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()),
+                            1 if to_tiled else 0, ctypes.c_void_p(stream.cuda_stream))
+    _check(rc, "qpgpu_relayout")
 
 
 # ----------------------------------------------------------------------------------------------

@@ -29,14 +29,26 @@ def _relerr(a, b):
     return float(np.max(r)) if r.size else 0.0
 
 
-def assert_parity(pr, label, max_iter=0, write_factor=False):
-    if not qpgpu.kernel_name(pr.n, pr.p, pr.m):
-        pytest.skip(f"no kernel for {(pr.n, pr.p, pr.m)} yet")
+FAMILIES = (None, "lane", "subgroup")
+
+
+def covers(family, n, m):
+    if family == "lane":
+        return n <= 8 and m <= 16
+    if family == "subgroup":
+        return n <= 16 and m <= 64
+    return bool(qpgpu.kernel_name(n, 0, m))
+
+
+def assert_parity(pr, label, max_iter=0, write_factor=False, family=None, layout=None):
+    if not covers(family, pr.n, pr.m):
+        pytest.skip(f"family {family} does not cover {(pr.n, pr.p, pr.m)}")
     prc = qpgpu.Problems(pr.n, pr.p, pr.m, pr.G.copy(), pr.g0, pr.CE, pr.ce0, pr.CI, pr.ci0)
     cap = max_iter if max_iter > 0 else 1000 + 100 * (pr.n + pr.p + pr.m)
     xo, fo, so, io = oracle.solve_batch(prc, write_factor=write_factor, max_steps=cap)
     prg = qpgpu.Problems(pr.n, pr.p, pr.m, pr.G.copy(), pr.g0, pr.CE, pr.ce0, pr.CI, pr.ci0)
-    xg, fg, sg, ig = qpgpu.solve_batched_host(prg, write_factor=write_factor, max_iter=max_iter)
+    xg, fg, sg, ig = qpgpu.solve_batched_host(prg, write_factor=write_factor, max_iter=max_iter,
+                                              family=family, layout=layout)
     assert np.array_equal(so, sg), f"{label}: status differs at {np.where(so != sg)[0][:10]}"
     assert np.array_equal(io, ig), f"{label}: iteration count differs at {np.where(io != ig)[0][:10]}"
     ok = so != qpgpu.QP_NOT_POSITIVE_DEFINITE  # x untouched on that exit (reference throws)
@@ -60,35 +72,51 @@ def test_reference_kat_on_gpu(gpu):
         assert [[v.hex() for v in row] for row in G] == c["expect_G_after_hex"]
 
 
+@pytest.mark.parametrize("family", FAMILIES)
 @pytest.mark.parametrize("name,kind,n,p,m", qp_cases.CONFIGS)
-def test_config_parity(gpu, name, kind, n, p, m):
+def test_config_parity(gpu, name, kind, n, p, m, family):
     B = 4096 if n <= 16 else 512
-    assert_parity(qp_cases.make(kind, n, p, m, B), name)
+    assert_parity(qp_cases.make(kind, n, p, m, B), name, family=family)
 
 
+@pytest.mark.parametrize("layout", ["qp_major", "tiled64"])
+@pytest.mark.parametrize("family", FAMILIES)
 @pytest.mark.parametrize("name,pr", qp_cases.edge_cases(), ids=[c[0] for c in qp_cases.edge_cases()])
-def test_edge_parity(gpu, name, pr):
-    assert_parity(pr, name, write_factor=True)
+def test_edge_parity(gpu, name, pr, family, layout):
+    assert_parity(pr, name, write_factor=True, family=family, layout=layout)
 
 
-def test_batch_tail_and_odd_sizes(gpu):
+@pytest.mark.parametrize("family", FAMILIES)
+@pytest.mark.parametrize("name,kind,n,p,m", qp_cases.CONFIGS)
+def test_config_parity_tiled(gpu, name, kind, n, p, m, family):
+    B = 1000 if n <= 16 else 200
+    assert_parity(qp_cases.make(kind, n, p, m, B, seed=77), name, family=family, layout="tiled64")
+
+
+@pytest.mark.parametrize("family", FAMILIES)
+def test_batch_tail_and_odd_sizes(gpu, family):
     for B in (1, 3, 7, 9, 63, 65, 1001):
-        assert_parity(qp_cases.make("general", 7, 6, 14, B, seed=B), f"B={B}")
+        assert_parity(qp_cases.make("general", 7, 6, 14, B, seed=B), f"B={B}", family=family)
 
 
-def test_max_iter_cap_matches(gpu):
+@pytest.mark.parametrize("family", FAMILIES)
+def test_max_iter_cap_matches(gpu, family):
     pr = dict(qp_cases.edge_cases())["long_paths"]
-    st, _ = assert_parity(pr, "cap", max_iter=2)
+    st, _ = assert_parity(pr, "cap", max_iter=2, family=family)
     assert (st == qpgpu.QP_MAX_ITER).any()
 
 
-def test_full_size_c1_parity(gpu):
+@pytest.mark.parametrize("layout", ["qp_major", "tiled64"])
+@pytest.mark.parametrize("family", FAMILIES)
+def test_full_size_c1_parity(gpu, family, layout):
     """BASELINE.json metric config: 65 536 x (7, 6, 14), bitwise against the oracle."""
-    assert_parity(qpgpu.make_problems("general", 7, 6, 14, 0, 65536, seed=2026), "C1 full")
+    assert_parity(qpgpu.make_problems("general", 7, 6, 14, 0, 65536, seed=2026), "C1 full", family=family,
+                  layout=layout)
 
 
-def test_full_size_c2_parity(gpu):
-    assert_parity(qpgpu.make_problems("box", 7, 0, 14, 0, 65536, seed=2026), "C2 full")
+@pytest.mark.parametrize("family", FAMILIES)
+def test_full_size_c2_parity(gpu, family):
+    assert_parity(qpgpu.make_problems("box", 7, 0, 14, 0, 65536, seed=2026), "C2 full", family=family)
 
 
 def test_device_api_matches_host_api(gpu):
@@ -117,3 +145,19 @@ def test_python_mirror_raises_like_reference(gpu):
     f, x = qpgpu.solve_quadprog(np.eye(2), np.zeros(2), np.zeros((2, 0)), [],
                                 [[1., -1.], [0., 0.]], [-1., 0.])
     assert f == float("inf")
+
+
+def test_device_relayout_roundtrip(gpu):
+    import torch
+
+    rng = np.random.default_rng(3)
+    for B, E in ((1, 5), (65, 98), (1000, 49), (4096, 33)):
+        a = rng.standard_normal((B, E))
+        src = torch.from_numpy(a).to("cuda:0")
+        t = torch.zeros((B + 63) // 64 * 64 * E, dtype=torch.float64, device="cuda:0")
+        qpgpu.relayout(src, t, B, E, True)
+        back = torch.zeros_like(src)
+        qpgpu.relayout(t, back, B, E, False)
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy(), qpgpu.to_tiled64(a))
+        assert np.array_equal(back.cpu().numpy(), a)

@@ -57,6 +57,8 @@ def test_invalid_arguments():
     assert qpgpu.LIB.qpgpu_solve_batched(ctypes.byref(d), *([z] * 11)) == qpgpu.ERR_INVALID_ARGUMENT
     d = qpgpu.ProblemDesc(7, 6, 14, 0, 4, 0x80, 0)
     assert qpgpu.LIB.qpgpu_solve_batched(ctypes.byref(d), *([z] * 11)) == qpgpu.ERR_INVALID_ARGUMENT
+    d = qpgpu.ProblemDesc(7, 6, 14, 0, 4, 0, 7)  # unknown layout
+    assert qpgpu.LIB.qpgpu_solve_batched(ctypes.byref(d), *([z] * 11)) == qpgpu.ERR_INVALID_ARGUMENT
     d = qpgpu.ProblemDesc(7, 6, 14, 0, 0, 0, 0)  # empty batch is a no-op
     assert qpgpu.LIB.qpgpu_solve_batched(ctypes.byref(d), *([z] * 11)) == qpgpu.SUCCESS
 
@@ -94,3 +96,15 @@ def test_python_mirror_dimension_errors():
         qpgpu.solve_quadprog(np.eye(2), np.zeros(2), np.ones((2, 1)), [1.0, 2.0], np.zeros((2, 0)), [])
     with pytest.raises(ValueError, match="ci0 is incompatible"):
         qpgpu.solve_quadprog(np.eye(2), np.zeros(2), np.zeros((2, 0)), [], np.ones((2, 2)), [1.0])
+
+
+def test_tiled64_roundtrip_host():
+    rng = np.random.default_rng(0)
+    for B in (1, 63, 64, 65, 200):
+        a = rng.standard_normal((B, 7, 3))
+        t = qpgpu.to_tiled64(a)
+        assert t.size == (B + 63) // 64 * 64 * 21
+        # element e of QP b at (b//64)*64*E + e*64 + b%64
+        b, e = B - 1, 20
+        assert t[(b // 64) * 64 * 21 + e * 64 + b % 64] == a.reshape(B, 21)[b, e]
+        assert np.array_equal(qpgpu.from_tiled64(t, B, (7, 3)), a)

@@ -28,12 +28,21 @@ for s in $STEPS; do
     pytest) run pytest 900 python -m pytest tests -m gpu -q -rf ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
+    benchfam)
+      for f in ${FAMILIES:-lane subgroup}; do for l in qp_major tiled64; do run bench_${f}_$l 600 python bench.py --family $f --layout $l --no-cpu; done; done ;;
     benchall)
       for c in C1 C2 mgqp; do run bench_$c 600 python bench.py --config $c --no-cpu; done ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c1 -- python3 bench.py --steps 20 --warmup 5 --no-cpu ;;
     pmc)
       run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu
       run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu ;;
+    listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;
+    sq)
+      for f in ${FAMILIES:-lane subgroup}; do
+        run sqA_$f 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d "$OUT/sqA_$f" -o c1 -- python3 bench.py --steps 3 --warmup 1 --no-cpu --family $f
+        run sqB_$f 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d "$OUT/sqB_$f" -o c1 -- python3 bench.py --steps 3 --warmup 1 --no-cpu --family $f
+        run sqC_$f 600 rocprofv3 --pmc SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH --output-format csv -d "$OUT/sqC_$f" -o c1 -- python3 bench.py --steps 3 --warmup 1 --no-cpu --family $f
+      done ;;
   esac
 done
 echo "session $TAG done"
