@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=2026)
     ap.add_argument("--family", default=None, choices=["lane", "subgroup"],
                     help="force a kernel family (default: the dispatcher's choice)")
-    ap.add_argument("--layout", default="tiled64", choices=["qp_major", "tiled64"],
+    ap.add_argument("--layout", default="qp_major", choices=["qp_major", "tiled64"],
                     help="batch layout of the resident inputs (include/qpgpu.h)")
     ap.add_argument("--no-gather", action="store_true", help="skip the rank-0 result gather (N>1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")

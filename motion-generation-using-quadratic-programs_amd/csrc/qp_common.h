@@ -69,6 +69,17 @@ struct QpArgs {
   double* f;
   int32_t* status;
   int32_t* iters;
+  // diagnostic only (NULL in every product call): per-wave s_memtime stamps at phase
+  // boundaries, kStampSlots per wave, written by lane 0.  Never feeds an output.
+  uint64_t* stamps;
 };
+constexpr int kStampSlots = 8;
+
+__device__ __forceinline__ void qp_stamp(const QpArgs& a, int slot) {
+  if (a.stamps) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) a.stamps[(uint64_t)blockIdx.x * kStampSlots + slot] = t;
+  }
+}
 
 }  // namespace qpk

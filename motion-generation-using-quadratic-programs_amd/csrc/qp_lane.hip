@@ -1,22 +1,25 @@
-// qp_lane.hip — gfx950 batched Goldfarb–Idnani solver, ONE QP PER LANE (n <= 8).
+// qp_lane.hip — gfx950 batched Goldfarb–Idnani solver, ONE QP PER LANE (n <= 8, m <= 16).
 //
 // Restates solve_quadprog() (reference include/QuadProgpp/QuadProg++.hh:69-72; operation order
-// of the prebuilt libquadprog.a fixed in SURVEY.md §3.2) for 64 independent QPs per wavefront.
-// There is no cross-lane communication at all: every lane runs the whole algorithm for its own
-// QP, so the serial chains (Givens coefficients, back-substitutions, step lengths) are
-// executed once per QP instead of once per lane of a subgroup, which is the dominant cost at
-// these sizes.  Per-lane state placement (gfx950: 512 VGPR+AGPR per lane at 1 wave/SIMD,
-// 160 KiB LDS per CU):
-//   * J (= L^{-T}, n x n, touched by column pairs in every Givens sweep) lives in LDS,
-//     lane-interleaved (element (i,j) of lane l at [(i*NM + j)*64 + l]) so every access is a
-//     conflict-free ds_read/write_b64 and column indices may be run-time values;
-//   * R (upper triangle + first subdiagonal, the only entries the algorithm ever makes
-//     non-zero), x, z, d, np, u, r, A and s live in registers with compile-time indices;
-//   * G is factored in registers; CE, CI and ci0 are streamed from global memory (L2 / MALL)
-//     each time the algorithm reads them: the l1 scan walks CI row by row, which keeps every
-//     s[i] accumulating in the reference's j-ascending order.
+// of the prebuilt libquadprog.a fixed in SURVEY.md §3.2) for the 64 QPs of one wavefront.
+//
+// Why one QP per lane: at these sizes the cost is the serial chain of every QP (Givens
+// coefficients = 4 IEEE divisions + 1 sqrt each, back-substitutions, step lengths); running it
+// once per QP instead of once per lane of a subgroup cuts issued instructions ~4x versus
+// qp_small.hip.  State placement (gfx950: 512 VGPR+AGPR per lane at 1 wave/SIMD, 160 KiB LDS
+// per CU = 40 KiB per wave at 4 waves/CU):
+//   * J (= L^{-T}), R (upper triangle + first subdiagonal, the only entries the algorithm makes
+//     non-zero), x, z, d, np, u, r, A, s live in registers, indexed only with compile-time
+//     indices (fully unrolled loops with run-time predicates);
+//   * every input block is brought in by COOPERATIVE, coalesced wave loads of the wave's 64
+//     contiguous QP blocks into a 40 KiB LDS staging buffer, then read per lane from LDS
+//     (QP-major: lane t at [t*(c|1) + k], odd stride = conflict-free ds_read_b64; TILED64:
+//     [k*64 + t]).  The l1 scan re-stages CI in row chunks each time any lane of the wave
+//     scans, so the main loop is wave-uniform (lanes that are done ride along predicated).
 // IEEE binary64 throughout, no contraction: results are bitwise identical to the CPU
 // restatement (oracle/qp_oracle.c), which tests/ check.
+#include <cstdlib>
+
 #include "qp_common.h"
 
 namespace qpk {
@@ -52,45 +55,121 @@ struct RIdx {
   }
 };
 
-template <int NM, int MM, int T>
+constexpr int kStage = 5120;  // staging buffer, doubles (40 KiB: 4 waves per CU)
+
+__device__ __forceinline__ bool wave_any(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
+
+template <int NM, int MM, int T, bool EXACT>
 __global__ void __launch_bounds__(64) qp_lane_kernel(const QpArgs a) {
   static_assert(MM <= 64, "bitmask bookkeeping holds m <= 64");
+  static_assert(64 * (NM * NM | 1) + 64 * (NM | 1) <= kStage, "G + g0 must fit one stage");
   using RI = RIdx<NM>;
-  __shared__ double Jl[NM * NM * 64];
+  // scan staging: TILED64 rounds of RPR CI rows (+ ci0 in the last round); QP-major rounds
+  // of QPR whole QPs (CI + ci0 blocks)
+  constexpr int RPR = (kStage - (64 * MM + 127) / 128 * 128) / (64 * MM);
+  constexpr int NROUND = (NM + RPR - 1) / RPR;
+  static_assert(RPR >= 1, "stage buffer too small for one CI row");
+  constexpr int QPR = ((64 * (NM * MM + MM) + 127) / 128 * 128 <= kStage) ? 64 : 32;
+  static_assert((QPR * NM * MM + 127) / 128 * 128 + QPR * MM <= kStage, "CI half-tile must fit");
+  // LDS per wave: J region + rollback region (40 KiB at NM = 7: 4 waves/CU)
+  constexpr int STAGE_MIN = (64 * NM * NM + 127) / 128 * 128 + 64 * (3 * NM + 2);
+  constexpr int STAGE = STAGE_MIN > kStage ? STAGE_MIN : kStage;
+  __shared__ double sbuf[STAGE];
 
   const int lane = threadIdx.x;
-  const int64_t b = (int64_t)blockIdx.x * 64 + lane;
-  if (b >= a.batch) return;  // lanes are fully independent
+  const int64_t b0 = (int64_t)blockIdx.x * 64;
+  const int64_t b = b0 + lane;
+  const int valid = (int)min<int64_t>(64, a.batch - b0);
+  const bool live = lane < valid;
 
-#define JL(i, j) Jl[((i) * NM + (j)) * 64 + lane]
-
-  const int n = a.n, p = a.p, m = a.m;
+  // EXACT: the shape is (NM, *, MM), so every element offset is a compile-time constant
+  const int n = EXACT ? NM : a.n;
+  const int m = EXACT ? MM : a.m;
+  const int p = a.p;
   const double inf = dinf();
-  // per-QP views: element e of each block is at <base> + e*T (qbase, include/qpgpu.h layouts)
-  const double* __restrict__ CIb = a.CI + qbase<T>(b, n * m);
-  const double* __restrict__ ci0b = a.ci0 + qbase<T>(b, m);
-  const double* __restrict__ CEb = a.CE + qbase<T>(b, n * p);
-  const double* __restrict__ ce0b = a.ce0 + qbase<T>(b, p);
+
+  // The wave's 64 QPs occupy [X + b0*E, X + (b0+64)*E) in both layouts (TILED64 arrays hold
+  // whole tiles, so its waves are always full).  Staging copies a contiguous span of that
+  // range into sbuf with LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave-instruction, no
+  // VGPRs, everything in flight at once); a partial last QP-major wave copies per lane.
+  const bool full = (T == 64) || (valid == 64);
+  auto copy_span = [&](const double* src, int nd, int off) {  // nd even, full waves only
+#pragma unroll 4
+    for (int k = 0; k < nd; k += 128) {
+      const int e = k + 2 * lane;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(e < nd ? src + e : src),
+          (__attribute__((address_space(3))) void*)(sbuf + off + k), 16, 0, 0);
+    }
+  };
+  // whole tile of X (E doubles per QP) -> sbuf[off...]
+  auto stage_all = [&](const double* X, int E, int off) {
+    if (full) {
+      copy_span(X + b0 * (int64_t)E, 64 * E, off);
+    } else if (live) {
+      const double* src = X + b * (int64_t)E;
+      for (int e = 0; e < E; e++) sbuf[off + lane * E + e] = src[e];
+    }
+  };
+  auto rd_all = [&](int off, int E, int k) -> double {
+    if constexpr (T == 64)
+      return sbuf[off + k * 64 + lane];
+    else
+      return sbuf[off + lane * E + k];
+  };
+  auto view = [&](double* X, int E) -> double* {
+    if constexpr (T == 64)
+      return X + b0 * (int64_t)E + lane;
+    else
+      return X + b * (int64_t)E;
+  };
 
   int status = QPGPU_QP_OK;
   double fval = 0.0;
   int iter = 0;
-  bool write_x = true;
   double xv[NM];
 #pragma unroll
   for (int i = 0; i < NM; i++) xv[i] = 0.0;
   double c1 = 0.0, c2 = 0.0;
+  // LDS regions: JA = J (lane-interleaved, element (i,j) of lane l at [(i*NM+j)*64 + l]),
+  // which first serves as the staging area for G and then CE; RB = g0 staging, then the
+  // rollback copies x_old / u_old / A_old.  Keeping J and the rollback state out of VGPRs
+  // leaves the compiler room to keep memory operations in flight.
+  constexpr int JA = (64 * NM * NM + 127) / 128 * 128;
+  constexpr int RB = JA;
+  constexpr int RB_U = RB + 64 * NM, RB_A = RB_U + 64 * (NM + 1);
+  static_assert(RB_A + 64 * (NM + 1) <= STAGE, "LDS regions exceed the stage buffer");
+#define Jr_(i, j) sbuf[((i) * NM + (j)) * 64 + lane]
+  double CEr[NM][NM], ce0r[NM];  // CEr[i][j] = CE[j][i] (column i = equality constraint i)
+  qp_stamp(a, 0);
 
-  // ---------------------------------------------------------------- setup (registers)
+  // ---------------------------------------------------------------- setup
   bool chol_ok = true;
   double bad_sum = 0.0;
   {
     double Gr[NM][NM];
-    const double* Gb = a.G + qbase<T>(b, n * n);
+    // round A: G and g0
+    const int offg0 = RB;
+    stage_all(a.G, n * n, 0);
+    stage_all(a.g0, n, offg0);
+    __syncthreads();
+    double g0v[NM];
 #pragma unroll
-    for (int i = 0; i < NM; i++)
+    for (int i = 0; i < NM; i++) {
 #pragma unroll
-      for (int j = 0; j < NM; j++) Gr[i][j] = (i < n && j < n) ? Gb[(i * n + j) * T] : 0.0;
+      for (int j = 0; j < NM; j++) Gr[i][j] = (i < n && j < n) ? rd_all(0, n * n, i * n + j) : 0.0;
+      g0v[i] = (i < n) ? rd_all(offg0, n, i) : 0.0;
+    }
+    __syncthreads();
+    // round B: CE and ce0 (equality phase), issued now so they land during the Cholesky
+    if (p > 0) {
+      const int np_ = n * p;
+      const int offc = (64 * np_ + 127) / 128 * 128;
+      if (offc + 64 * p <= STAGE) {
+        stage_all(a.CE, np_, 0);
+        stage_all(a.ce0, p, offc);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NM; i++)
       if (i < n) c1 += Gr[i][i];
@@ -120,41 +199,73 @@ __global__ void __launch_bounds__(64) qp_lane_kernel(const QpArgs a) {
         }
       }
     }
-    if (a.flags & QPGPU_FLAG_WRITE_FACTOR) {
-      double* Gw = a.G + qbase<T>(b, n * n);
+    if ((a.flags & QPGPU_FLAG_WRITE_FACTOR) && live) {
+      double* Gw = view(a.G, n * n);
 #pragma unroll
       for (int i = 0; i < NM; i++)
 #pragma unroll
         for (int j = 0; j < NM; j++)
           if (i < n && j < n) Gw[(i * n + j) * T] = Gr[i][j];
     }
+    // round B lands: CE columns into registers (before J overwrites the JA region)
+    if (p > 0) {
+      const int np_ = n * p;
+      const int offc = (64 * np_ + 127) / 128 * 128;
+      const bool staged = offc + 64 * p <= STAGE;
+      __syncthreads();
+  #pragma unroll
+      for (int i = 0; i < NM; i++) {
+  #pragma unroll
+        for (int j = 0; j < NM; j++) {
+          double v = 0.0;
+          if (live && i < p && j < n)
+            v = staged ? rd_all(0, np_, j * p + i) : view(const_cast<double*>(a.CE), np_)[(j * p + i) * T];
+          CEr[i][j] = v;
+        }
+        double c0 = 0.0;
+        if (live && i < p) c0 = staged ? rd_all(offc, p, i) : view(const_cast<double*>(a.ce0), p)[i * T];
+        ce0r[i] = c0;
+      }
+      __syncthreads();
+    }
     if (chol_ok) {
-      // J = L^{-T}: row i of J = L^{-1} e_i (forward_elimination); c2 = trace(J)
+      // J = L^{-T}: row r of J = L^{-1} e_r (forward_elimination); c2 = trace(J).
+      // With a finite L the first r entries of L^{-1} e_r are exactly +0.0 (0.0 - L*(+0) and
+      // 0.0 / L stay +0.0) and contribute exact zeros to later sums, so they are skipped: same
+      // bits, ~40% fewer divisions.  A non-finite L (NaN inputs) takes the literal path.
+      bool lfin = true;
 #pragma unroll
-      for (int r = 0; r < NM; r++) {
-        if (r < n) {
+      for (int i = 0; i < NM; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++)
+          if (i < n) lfin = lfin && (fabs(Gr[i][j]) < inf);
+      auto build_j = [&](const bool skip) {
+#pragma unroll
+        for (int r = 0; r < NM; r++) {
           double y[NM];
 #pragma unroll
           for (int i = 0; i < NM; i++) {
             double v = 0.0;
-            if (i < n) {
+            if (r < n && i < n && !(skip && i < r)) {
               v = (i == r) ? 1.0 : 0.0;
 #pragma unroll
-              for (int j = 0; j < i; j++) v -= Gr[i][j] * y[j];
+              for (int j = 0; j < i; j++)
+                if (!(skip && j < r)) v -= Gr[i][j] * y[j];
               v = v / Gr[i][i];
             }
             y[i] = v;
           }
 #pragma unroll
-          for (int j = 0; j < NM; j++) JL(r, j) = y[j];
-          c2 += y[r];
+          for (int j = 0; j < NM; j++) Jr_(r, j) = y[j];
+          if (r < n) c2 += y[r];
         }
-      }
+      };
+      if (lfin)
+        build_j(true);
+      else
+        build_j(false);
       // cholesky_solve (@.text+0x31a2): x = -G^{-1} g0
-      double g0v[NM], y[NM];
-      const double* g0b = a.g0 + qbase<T>(b, n);
-#pragma unroll
-      for (int i = 0; i < NM; i++) g0v[i] = (i < n) ? g0b[i * T] : 0.0;
+      double y[NM];
 #pragma unroll
       for (int i = 0; i < NM; i++) {
         double v = 0.0;
@@ -184,394 +295,513 @@ __global__ void __launch_bounds__(64) qp_lane_kernel(const QpArgs a) {
       fval = 0.5 * fval;
     }
   }
-
+  qp_stamp(a, 1);
   if (!chol_ok) {
     status = QPGPU_QP_NOT_POSITIVE_DEFINITE;
     fval = bad_sum;
-    write_x = false;
-  } else {
-    // ---------------------------------------------------------------- state
-    double Rv[RI::SIZE];
+  }
+  const bool ok_lane = live && chol_ok;
+
+  // ---------------------------------------------------------------- state
+  double Rv[RI::SIZE];
 #pragma unroll
-    for (int i = 0; i < RI::SIZE; i++) Rv[i] = 0.0;
-    double dv[NM], zv[NM], npv[NM], uv[NM + 1], rv[NM];
-    int Av[NM + 1];
+  for (int i = 0; i < RI::SIZE; i++) Rv[i] = 0.0;
+  double dv[NM], zv[NM], npv[NM], uv[NM + 1], rv[NM];
+  int Av[NM + 1];
 #pragma unroll
-    for (int i = 0; i < NM; i++) dv[i] = zv[i] = npv[i] = rv[i] = 0.0;
+  for (int i = 0; i < NM; i++) dv[i] = zv[i] = npv[i] = rv[i] = 0.0;
 #pragma unroll
-    for (int i = 0; i <= NM; i++) {
-      uv[i] = 0.0;
-      Av[i] = 0;
-    }
-    double R_norm = 1.0;
-    int iq = 0;
+  for (int i = 0; i <= NM; i++) {
+    uv[i] = 0.0;
+    Av[i] = 0;
+  }
+  double R_norm = 1.0;
+  int iq = 0;
 
     auto compute_d = [&]() {
 #pragma unroll
-      for (int c = 0; c < NM; c++) {
-        double s = 0.0;
-#pragma unroll
-        for (int j = 0; j < NM; j++)
-          if (j < n) s += JL(j, c) * npv[j];
-        dv[c] = s;
-      }
-    };
-    auto update_z = [&]() {
-#pragma unroll
-      for (int r = 0; r < NM; r++) {
-        double z = 0.0;
-#pragma unroll
-        for (int j = 0; j < NM; j++)
-          if (j >= iq && j < n) z += JL(r, j) * dv[j];
-        zv[r] = z;
-      }
-    };
-    auto update_r = [&]() {
-#pragma unroll
-      for (int i = NM - 1; i >= 0; i--) {
-        if (i < iq) {
-          double s = 0.0;
-#pragma unroll
-          for (int j = i + 1; j < NM; j++)
-            if (j < iq) s += Rv[RI::at(i, j)] * rv[j];
-          rv[i] = (dv[i] - s) / Rv[RI::at(i, i)];
-        }
-      }
-    };
-    auto add_constraint = [&]() -> bool {
-      if (iq >= n) return false;  // reference UB (p > n); reported as dependent
-#pragma unroll
-      for (int j = NM - 1; j >= 1; j--) {
-        if (j <= n - 1 && j >= iq + 1) {
-          double cc = dv[j - 1], ss = dv[j];
-          const double h = qp_distance(cc, ss);
-          if (!(fabs(h) < kEps)) {
-            dv[j] = 0.0;
-            ss = ss / h;
-            cc = cc / h;
-            if (cc < 0.0) {
-              cc = -cc;
-              ss = -ss;
-              dv[j - 1] = -h;
-            } else {
-              dv[j - 1] = h;
-            }
-            const double xny = ss / (1.0 + cc);
-#pragma unroll
-            for (int k = 0; k < NM; k++)
-              if (k < n) {
-                const double t1 = JL(k, j - 1), t2 = JL(k, j);
-                const double n1 = t1 * cc + t2 * ss;
-                JL(k, j - 1) = n1;
-                JL(k, j) = xny * (t1 + n1) - t2;
-              }
-          }
-        }
-      }
-      iq++;
-      // R[:iq, iq-1] = d[:iq]
-#pragma unroll
-      for (int c = 0; c < NM; c++)
-#pragma unroll
-        for (int i = 0; i <= c; i++) {
-          const bool w = (c == iq - 1);
-          Rv[RI::at(i, c)] = w ? dv[i] : Rv[RI::at(i, c)];
-        }
-      const double dd = fabs(lsel<NM>(dv, iq - 1));
-      if (dd <= kEps * R_norm) return false;
-      R_norm = (R_norm < dd) ? dd : R_norm;
-      return true;
-    };
-    auto delete_constraint = [&](int l) {
-      int qq = 0;
-      bool found = false;
-#pragma unroll
-      for (int k = 0; k <= NM; k++)
-        if (!found && k >= p && k < iq && Av[k] == l) {
-          qq = k;
-          found = true;
-        }
-#pragma unroll
-      for (int i = 0; i < NM; i++)
-        if (i >= qq && i < iq - 1) {
-          Av[i] = Av[i + 1];
-          uv[i] = uv[i + 1];
-        }
-      // shift R columns left from qq (only upper + subdiagonal entries exist)
-#pragma unroll
-      for (int c = 0; c < NM - 1; c++) {
-        const bool sh = (c >= qq && c < iq - 1);
-#pragma unroll
-        for (int r = 0; r <= c + 1 && r < NM; r++) {
-          // destination R[r][c] (upper or subdiagonal), source R[r][c+1] (upper)
-          Rv[RI::at(r, c)] = sh ? Rv[RI::at(r, c + 1)] : Rv[RI::at(r, c)];
-        }
-      }
-      {
-        const int aiq = lsel<NM + 1>(Av, iq);
-        const double uiq = lsel<NM + 1>(uv, iq);
-        lput<NM + 1>(Av, iq - 1, aiq);
-        lput<NM + 1>(uv, iq - 1, uiq);
-        lput<NM + 1>(Av, iq, 0);
-        lput<NM + 1>(uv, iq, 0.0);
-      }
-      // R[j][iq-1] = 0 for j < iq
-#pragma unroll
-      for (int c = 0; c < NM; c++)
-#pragma unroll
-        for (int r = 0; r <= c + 1 && r < NM; r++) {
-          const bool z = (c == iq - 1) && (r < iq);
-          Rv[RI::at(r, c)] = z ? 0.0 : Rv[RI::at(r, c)];
-        }
-      iq--;
-      if (iq == 0) return;
-#pragma unroll
-      for (int j = 0; j < NM - 1; j++) {
-        if (j >= qq && j < iq) {
-          double cc = Rv[RI::at(j, j)], ss = Rv[RI::at(j + 1, j)];
-          const double h = qp_distance(cc, ss);
-          if (!(fabs(h) < kEps)) {
-            cc = cc / h;
-            ss = ss / h;
-            Rv[RI::at(j + 1, j)] = 0.0;
-            if (cc < 0.0) {
-              Rv[RI::at(j, j)] = -h;
-              cc = -cc;
-              ss = -ss;
-            } else {
-              Rv[RI::at(j, j)] = h;
-            }
-            const double xny = ss / (1.0 + cc);
-#pragma unroll
-            for (int k = j + 1; k < NM; k++)
-              if (k < iq) {
-                const double t1 = Rv[RI::at(j, k)], t2 = Rv[RI::at(j + 1, k)];
-                const double r1 = t1 * cc + t2 * ss;
-                Rv[RI::at(j, k)] = r1;
-                Rv[RI::at(j + 1, k)] = xny * (t1 + r1) - t2;
-              }
-#pragma unroll
-            for (int k = 0; k < NM; k++)
-              if (k < n) {
-                const double t1 = JL(k, j), t2 = JL(k, j + 1);
-                const double n1 = t1 * cc + t2 * ss;
-                JL(k, j) = n1;
-                JL(k, j + 1) = xny * (n1 + t1) - t2;
-              }
-          }
-        }
-      }
-    };
-    auto dot = [&](const double(&u_)[NM], const double(&v_)[NM]) -> double {
+    for (int c = 0; c < NM; c++) {
       double s = 0.0;
 #pragma unroll
-      for (int i = 0; i < NM; i++)
-        if (i < n) s += u_[i] * v_[i];
-      return s;
-    };
+      for (int j = 0; j < NM; j++)
+        if (j < n) s += Jr_(j, c) * npv[j];
+      dv[c] = s;
+    }
+  };
+  auto update_z = [&]() {
+#pragma unroll
+    for (int r = 0; r < NM; r++) {
+      double z = 0.0;
+#pragma unroll
+      for (int j = 0; j < NM; j++)
+        if (j >= iq && j < n) z += Jr_(r, j) * dv[j];
+      zv[r] = z;
+    }
+  };
+  auto update_r = [&]() {
+#pragma unroll
+    for (int i = NM - 1; i >= 0; i--) {
+      if (i < iq) {
+        double s = 0.0;
+#pragma unroll
+        for (int j = i + 1; j < NM; j++)
+          if (j < iq) s += Rv[RI::at(i, j)] * rv[j];
+        rv[i] = (dv[i] - s) / Rv[RI::at(i, i)];
+      }
+    }
+  };
+  auto add_constraint = [&]() -> bool {
+    if (iq >= n) return false;  // reference UB (p > n); reported as dependent
+#pragma unroll
+    for (int j = NM - 1; j >= 1; j--) {
+      if (j <= n - 1 && j >= iq + 1) {
+        double cc = dv[j - 1], ss = dv[j];
+        const double h = qp_distance(cc, ss);
+        if (!(fabs(h) < kEps)) {
+          dv[j] = 0.0;
+          ss = ss / h;
+          cc = cc / h;
+          if (cc < 0.0) {
+            cc = -cc;
+            ss = -ss;
+            dv[j - 1] = -h;
+          } else {
+            dv[j - 1] = h;
+          }
+          const double xny = ss / (1.0 + cc);
+#pragma unroll
+          for (int k = 0; k < NM; k++)
+            if (k < n) {
+              const double t1 = Jr_(k, j - 1), t2 = Jr_(k, j);
+              const double n1 = t1 * cc + t2 * ss;
+              Jr_(k, j - 1) = n1;
+              Jr_(k, j) = xny * (t1 + n1) - t2;
+            }
+        }
+      }
+    }
+    iq++;
+    // R[:iq, iq-1] = d[:iq]
+#pragma unroll
+    for (int c = 0; c < NM; c++)
+#pragma unroll
+      for (int i = 0; i <= c; i++) {
+        const bool w = (c == iq - 1);
+        Rv[RI::at(i, c)] = w ? dv[i] : Rv[RI::at(i, c)];
+      }
+    const double dd = fabs(lsel<NM>(dv, iq - 1));
+    if (dd <= kEps * R_norm) return false;
+    R_norm = (R_norm < dd) ? dd : R_norm;
+    return true;
+  };
+  auto delete_constraint = [&](int l) {
+    int qq = 0;
+    bool found = false;
+#pragma unroll
+    for (int k = 0; k <= NM; k++)
+      if (!found && k >= p && k < iq && Av[k] == l) {
+        qq = k;
+        found = true;
+      }
+#pragma unroll
+    for (int i = 0; i < NM; i++)
+      if (i >= qq && i < iq - 1) {
+        Av[i] = Av[i + 1];
+        uv[i] = uv[i + 1];
+      }
+    // shift R columns left from qq (only upper + subdiagonal entries exist)
+#pragma unroll
+    for (int c = 0; c < NM - 1; c++) {
+      const bool sh = (c >= qq && c < iq - 1);
+#pragma unroll
+      for (int r = 0; r <= c + 1 && r < NM; r++) {
+        // destination R[r][c] (upper or subdiagonal), source R[r][c+1] (upper)
+        Rv[RI::at(r, c)] = sh ? Rv[RI::at(r, c + 1)] : Rv[RI::at(r, c)];
+      }
+    }
+    {
+      const int aiq = lsel<NM + 1>(Av, iq);
+      const double uiq = lsel<NM + 1>(uv, iq);
+      lput<NM + 1>(Av, iq - 1, aiq);
+      lput<NM + 1>(uv, iq - 1, uiq);
+      lput<NM + 1>(Av, iq, 0);
+      lput<NM + 1>(uv, iq, 0.0);
+    }
+    // R[j][iq-1] = 0 for j < iq
+#pragma unroll
+    for (int c = 0; c < NM; c++)
+#pragma unroll
+      for (int r = 0; r <= c + 1 && r < NM; r++) {
+        const bool z = (c == iq - 1) && (r < iq);
+        Rv[RI::at(r, c)] = z ? 0.0 : Rv[RI::at(r, c)];
+      }
+    iq--;
+    if (iq == 0) return;
+#pragma unroll
+    for (int j = 0; j < NM - 1; j++) {
+      if (j >= qq && j < iq) {
+        double cc = Rv[RI::at(j, j)], ss = Rv[RI::at(j + 1, j)];
+        const double h = qp_distance(cc, ss);
+        if (!(fabs(h) < kEps)) {
+          cc = cc / h;
+          ss = ss / h;
+          Rv[RI::at(j + 1, j)] = 0.0;
+          if (cc < 0.0) {
+            Rv[RI::at(j, j)] = -h;
+            cc = -cc;
+            ss = -ss;
+          } else {
+            Rv[RI::at(j, j)] = h;
+          }
+          const double xny = ss / (1.0 + cc);
+#pragma unroll
+          for (int k = j + 1; k < NM; k++)
+            if (k < iq) {
+              const double t1 = Rv[RI::at(j, k)], t2 = Rv[RI::at(j + 1, k)];
+              const double r1 = t1 * cc + t2 * ss;
+              Rv[RI::at(j, k)] = r1;
+              Rv[RI::at(j + 1, k)] = xny * (t1 + r1) - t2;
+            }
+#pragma unroll
+          for (int k = 0; k < NM; k++)
+            if (k < n) {
+              const double t1 = Jr_(k, j), t2 = Jr_(k, j + 1);
+              const double n1 = t1 * cc + t2 * ss;
+              Jr_(k, j) = n1;
+              Jr_(k, j + 1) = xny * (n1 + t1) - t2;
+            }
+        }
+      }
+    }
+  };
+  auto dot = [&](const double(&u_)[NM], const double(&v_)[NM]) -> double {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < NM; i++)
+      if (i < n) s += u_[i] * v_[i];
+    return s;
+  };
 
     // ---------------------------------------------------------------- equality phase
-    bool done = false;
-    for (int i = 0; i < p && !done; i++) {
+  // Fully unrolled: in step i the active-set size iq equals i (every earlier step added a
+  // constraint, or the phase stopped), so pinning iq to the compile-time i folds every
+  // iq-predicate of compute_d / update_z / update_r / add_constraint.
+  bool done = !ok_lane;
 #pragma unroll
-      for (int j = 0; j < NM; j++) npv[j] = (j < n) ? CEb[(j * p + i) * T] : 0.0;
+  for (int i = 0; i <= NM; i++) {
+    if (i < p && !done) {
+      iq = i;
+      double c0;
+      if (i < NM) {
+#pragma unroll
+        for (int j = 0; j < NM; j++) npv[j] = CEr[i][j];
+        c0 = ce0r[i];
+      } else {  // p > n: the step that reports "dependent" (reference UB, see oracle)
+        const double* CEb = view(const_cast<double*>(a.CE), n * p);
+#pragma unroll
+        for (int j = 0; j < NM; j++) npv[j] = (j < n) ? CEb[(j * p + i) * T] : 0.0;
+        c0 = view(const_cast<double*>(a.ce0), p)[i * T];
+      }
       compute_d();
       update_z();
       update_r();
       double t2 = 0.0;
       const double zz = dot(zv, zv);
       const double znp = dot(zv, npv);
-      if (fabs(zz) > kEps) t2 = (-dot(npv, xv) - ce0b[i * T]) / znp;
+      if (fabs(zz) > kEps) t2 = (-dot(npv, xv) - c0) / znp;
 #pragma unroll
       for (int k = 0; k < NM; k++) xv[k] += t2 * zv[k];
-      lput<NM + 1>(uv, iq, t2);
+      uv[i < NM + 1 ? i : NM] = t2;
 #pragma unroll
       for (int k = 0; k < NM; k++)
-        if (k < iq) uv[k] -= t2 * rv[k];
+        if (k < i) uv[k] -= t2 * rv[k];
       fval += 0.5 * (t2 * t2) * znp;
-      lput<NM + 1>(Av, i, -i - 1);
+      Av[i < NM + 1 ? i : NM] = -i - 1;
       if (!add_constraint()) {
         status = QPGPU_QP_DEPENDENT;
         done = true;
       }
     }
+  }
+  qp_stamp(a, 2);
 
-    // ---------------------------------------------------------------- active-set loop
-    if (!done) {
-      double sv[MM];
+  // ---------------------------------------------------------------- active-set loop
+  // Wave-uniform loop: every lane stays until all 64 are done, so the cooperative CI staging
+  // and its barriers are reached by the whole wave; per-lane work is predicated on `active`.
+  {
+    double sv[MM];
 #pragma unroll
-      for (int i = 0; i < MM; i++) sv[i] = 0.0;
-      double xold[NM], uold[NM + 1];
-      int aold[NM + 1];
-#pragma unroll
-      for (int i = 0; i < NM; i++) xold[i] = 0.0;
-#pragma unroll
-      for (int i = 0; i <= NM; i++) {
-        uold[i] = 0.0;
-        aold[i] = 0;
-      }
-      uint64_t act = 0;   // bit c set <=> iai[c] == -1
-      uint64_t excl = 0;  // bit c set <=> iaexcl[c] == false
-      int ip = 0, steps = 0;
-      double ss = 0.0;
-      bool need_scan = true, need_select = true;
-      const int max_steps = a.max_steps;
-      while (true) {
-        if (need_scan) {  // ---- l1
+    for (int i = 0; i < MM; i++) sv[i] = 0.0;
+#define XOLD(i) sbuf[RB + (i) * 64 + lane]
+#define UOLD(i) sbuf[RB_U + (i) * 64 + lane]
+#define AOLD(i) sbuf[RB_A + (i) * 64 + lane]
+    uint64_t act = 0;   // bit c set <=> iai[c] == -1
+    uint64_t excl = 0;  // bit c set <=> iaexcl[c] == false
+    int ip = 0, steps = 0;
+    double ss = 0.0, ci0ip = 0.0;
+    bool need_scan = true, need_select = true;
+    bool active = !done;
+    const int max_steps = a.max_steps;
+    const double* CIg = view(const_cast<double*>(a.CI), n * m);
+    const double* ci0g = view(const_cast<double*>(a.ci0), m);
+    // element loaders for this lane's CI / ci0 block.  TILED64: raw buffer loads off a
+    // wave-uniform descriptor (tile base) + one lane-offset VGPR + element offset in SGPR/imm,
+    // so no 64-bit address per element is kept live.
+    // descriptor inputs through readfirstlane so the compiler can PROVE them uniform (else
+    // it wraps every buffer op in a waterfall loop: guide T20)
+    auto uniform_ptr = [](const double* ptr) -> double* {
+      const uint64_t v = reinterpret_cast<uint64_t>(ptr);
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+      const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+      return reinterpret_cast<double*>(((uint64_t)hi << 32) | lo);
+    };
+    [[maybe_unused]] const auto rsCI = __builtin_amdgcn_make_buffer_rsrc(
+        uniform_ptr(a.CI + b0 * (int64_t)(n * m)), 0,
+        __builtin_amdgcn_readfirstlane(64 * n * m * 8), 0x00020000);
+    [[maybe_unused]] const auto rsci0 = __builtin_amdgcn_make_buffer_rsrc(
+        uniform_ptr(a.ci0 + b0 * (int64_t)m), 0, __builtin_amdgcn_readfirstlane(64 * m * 8),
+        0x00020000);
+    auto ldCI = [&](int e) -> double {
+      if constexpr (T == 64)
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsCI, lane * 8, e * 512, 0));
+      else
+        return CIg[e];
+    };
+    auto ldci0 = [&](int e) -> double {
+      if constexpr (T == 64)
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsci0, lane * 8, e * 512, 0));
+      else
+        return ci0g[e];
+    };
+    uint64_t tscan = 0, tsel = 0, nloop = 0;  // diagnostic stamps only
+    while (wave_any(active)) {
+      nloop++;
+      const uint64_t tl0 = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+      // ---- l1: s = CI^T x + ci0, CI staged in row chunks (each s[i] sums j ascending)
+      const bool do_scan = active && need_scan;
+      if (wave_any(do_scan)) {
+        double psi = 0.0;
+        if (do_scan) {
           iter++;
 #pragma unroll
           for (int k = 0; k < NM; k++)
             if (k >= p && k < iq) act |= 1ull << Av[k];
-          // s = CI^T x + ci0, walking CI row by row (each s[i] sums j ascending)
 #pragma unroll
           for (int i = 0; i < MM; i++) sv[i] = 0.0;
+        }
+        // per-lane loads by the scanning lanes only (a full-tile LDS stage per scan moves ~2x
+        // the bytes through the CU's load path and measured slower); TILED64 loads are
+        // coalesced 512-B rows through a wave-uniform buffer descriptor
+        // Software-pipelined two rows deep: row j+1's loads are issued (and fenced from the
+        // scheduler) before row j is consumed, so one memory latency covers two rows instead
+        // of the scheduler's one-load-at-a-time minimum-pressure order.
+        if (do_scan) {
+          double rowbuf[2][MM];
 #pragma unroll
-          for (int j = 0; j < NM; j++)
+          for (int i = 0; i < MM; i++) rowbuf[0][i] = (i < m) ? ldCI(i) : 0.0;
+#pragma unroll
+          for (int j = 0; j < NM; j++) {
+            if (j + 1 < NM) {
+#pragma unroll
+              for (int i = 0; i < MM; i++)
+                rowbuf[(j + 1) & 1][i] = (j + 1 < n && i < m) ? ldCI((j + 1) * m + i) : 0.0;
+            } else {
+#pragma unroll
+              for (int i = 0; i < MM; i++) rowbuf[(j + 1) & 1][i] = (i < m) ? ldci0(i) : 0.0;
+            }
+            __builtin_amdgcn_sched_barrier(0);
             if (j < n) {
               const double xj = xv[j];
 #pragma unroll
               for (int i = 0; i < MM; i++)
-                if (i < m) sv[i] += CIb[(j * m + i) * T] * xj;
+                if (i < m) sv[i] += rowbuf[j & 1][i] * xj;
             }
-          double psi = 0.0;
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if constexpr (!EXACT) {
+            if (n < NM) {  // ci0 was not fetched by the pipelined tail
+#pragma unroll
+              for (int i = 0; i < MM; i++) rowbuf[NM & 1][i] = (i < m) ? ldci0(i) : 0.0;
+            }
+          }
 #pragma unroll
           for (int i = 0; i < MM; i++)
             if (i < m) {
-              sv[i] += ci0b[i * T];
+              sv[i] += rowbuf[NM & 1][i];
               psi += (sv[i] < 0.0) ? sv[i] : 0.0;
             }
+        }
+        if (do_scan) {
           excl = 0;
           ss = 0.0;
           ip = 0;
-          if (fabs(psi) <= (double)m * kEps * c1 * c2 * 100.0) break;  // optimal
+          if (fabs(psi) <= (double)m * kEps * c1 * c2 * 100.0) {
+            active = false;  // optimal
+          } else {
 #pragma unroll
-          for (int i = 0; i < NM; i++) {
-            uold[i] = (i < iq) ? uv[i] : uold[i];
-            aold[i] = (i < iq) ? Av[i] : aold[i];
-            xold[i] = xv[i];
+            for (int i = 0; i < NM; i++) {
+              if (i < iq) {
+                UOLD(i) = uv[i];
+                AOLD(i) = (double)Av[i];
+              }
+              XOLD(i) = xv[i];
+            }
           }
         }
-        if (need_select) {  // ---- l2 (ss deliberately not reset: reference quirk)
+      }
+      const uint64_t tl1 = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+      // ---- l2: pick the most violated constraint (ss deliberately not reset: reference quirk)
+      if (active && need_select) {
 #pragma unroll
-          for (int i = 0; i < MM; i++)
-            if (i < m) {
-              const bool elig = !((act >> i) & 1ull) && !((excl >> i) & 1ull);
-              const bool take = sv[i] < ss && elig;
-              ss = take ? sv[i] : ss;
-              ip = take ? i : ip;
-            }
-          if (ss >= 0.0) break;  // optimal
+        for (int i = 0; i < MM; i++)
+          if (i < m) {
+            const bool elig = !((act >> i) & 1ull) && !((excl >> i) & 1ull);
+            const bool take = sv[i] < ss && elig;
+            ss = take ? sv[i] : ss;
+            ip = take ? i : ip;
+          }
+        if (ss >= 0.0) {
+          active = false;  // optimal
+        } else {
 #pragma unroll
-          for (int j = 0; j < NM; j++) npv[j] = (j < n) ? CIb[(j * m + ip) * T] : 0.0;
+          for (int j = 0; j < NM; j++) npv[j] = (j < n) ? ldCI(j * m + ip) : 0.0;
+          ci0ip = ldci0(ip);
           lput<NM + 1>(uv, iq, 0.0);
           lput<NM + 1>(Av, iq, ip);
         }
-        // ---- l2a
+      }
+      if (a.stamps) {
+        // make the select's loads part of the select span
+        const double sink = npv[0] + ci0ip;
+        asm volatile("" ::"v"(sink));
+        const uint64_t tl2 = __builtin_amdgcn_s_memtime();
+        tscan += tl1 - tl0;
+        tsel += tl2 - tl1;
+      }
+      // ---- l2a
+      if (active) {
         if (max_steps > 0 && ++steps > max_steps) {
           status = QPGPU_QP_MAX_ITER;
-          break;
-        }
-        compute_d();
-        update_z();
-        update_r();
-        int l = 0;
-        double t1 = inf;
-#pragma unroll
-        for (int k = 0; k < NM; k++)
-          if (k >= p && k < iq && rv[k] > 0.0) {
-            const double q_ = uv[k] / rv[k];
-            const bool take = q_ < t1;
-            t1 = take ? q_ : t1;
-            l = take ? opq_l(Av[k]) : l;
-          }
-        const double zz = dot(zv, zv);
-        const double znp = dot(zv, npv);
-        double t2;
-        if (fabs(zz) > kEps) {
-          t2 = -lsel<MM>(sv, ip) / znp;
-          if (t2 < 0) t2 = inf;  // Takano Akio patch
+          active = false;
         } else {
-          t2 = inf;
-        }
-        const double t = (t2 < t1) ? t2 : t1;
-        if (t >= inf) {
-          status = QPGPU_QP_INFEASIBLE;
-          fval = inf;
-          break;
-        }
-        if (t2 >= inf) {  // dual step only
+          compute_d();
+          update_z();
+          update_r();
+          int l = 0;
+          double t1 = inf;
 #pragma unroll
           for (int k = 0; k < NM; k++)
-            if (k < iq) uv[k] -= t * rv[k];
-          lput<NM + 1>(uv, iq, lsel<NM + 1>(uv, iq) + t);
-          act &= ~(1ull << l);
-          delete_constraint(l);
-          need_scan = need_select = false;
-          continue;
-        }
-#pragma unroll
-        for (int k = 0; k < NM; k++) xv[k] += t * zv[k];
-        fval += t * znp * (0.5 * t + lsel<NM + 1>(uv, iq));
-#pragma unroll
-        for (int k = 0; k < NM; k++)
-          if (k < iq) uv[k] -= t * rv[k];
-        lput<NM + 1>(uv, iq, lsel<NM + 1>(uv, iq) + t);
-        if (fabs(t - t2) < kEps) {  // full step
-          if (!add_constraint()) {
-            excl |= 1ull << ip;
-            delete_constraint(ip);
-            act = 0;
-#pragma unroll
-            for (int i = 0; i < NM; i++)
-              if (i >= p && i < iq) {
-                Av[i] = aold[i];
-                uv[i] = uold[i];
-                act |= 1ull << Av[i];
-              }
-#pragma unroll
-            for (int i = 0; i < NM; i++) xv[i] = xold[i];
-            need_scan = false;
-            need_select = true;
+            if (k >= p && k < iq && rv[k] > 0.0) {
+              const double q_ = uv[k] / rv[k];
+              const bool take = q_ < t1;
+              t1 = take ? q_ : t1;
+              l = take ? opq_l(Av[k]) : l;
+            }
+          const double zz = dot(zv, zv);
+          const double znp = dot(zv, npv);
+          double t2;
+          if (fabs(zz) > kEps) {
+            t2 = -lsel<MM>(sv, ip) / znp;
+            if (t2 < 0) t2 = inf;  // Takano Akio patch
           } else {
-            act |= 1ull << ip;
-            need_scan = need_select = true;
+            t2 = inf;
           }
-          continue;
-        }
-        // partial step: drop l, refresh s[ip]
-        act &= ~(1ull << l);
-        delete_constraint(l);
-        {
-          double s = 0.0;
+          const double t = (t2 < t1) ? t2 : t1;
+          if (t >= inf) {
+            status = QPGPU_QP_INFEASIBLE;
+            fval = inf;
+            active = false;
+          } else if (t2 >= inf) {  // dual step only
 #pragma unroll
-          for (int j = 0; j < NM; j++)
-            if (j < n) s += CIb[(j * m + ip) * T] * xv[j];
-          lput<MM>(sv, ip, s + ci0b[ip * T]);
+            for (int k = 0; k < NM; k++)
+              if (k < iq) uv[k] -= t * rv[k];
+            lput<NM + 1>(uv, iq, lsel<NM + 1>(uv, iq) + t);
+            act &= ~(1ull << l);
+            delete_constraint(l);
+            need_scan = need_select = false;
+          } else {
+#pragma unroll
+            for (int k = 0; k < NM; k++) xv[k] += t * zv[k];
+            fval += t * znp * (0.5 * t + lsel<NM + 1>(uv, iq));
+#pragma unroll
+            for (int k = 0; k < NM; k++)
+              if (k < iq) uv[k] -= t * rv[k];
+            lput<NM + 1>(uv, iq, lsel<NM + 1>(uv, iq) + t);
+            if (fabs(t - t2) < kEps) {  // full step
+              if (!add_constraint()) {
+                excl |= 1ull << ip;
+                delete_constraint(ip);
+                act = 0;
+#pragma unroll
+                for (int i = 0; i < NM; i++)
+                  if (i >= p && i < iq) {
+                    Av[i] = (int)AOLD(i);
+                    uv[i] = UOLD(i);
+                    act |= 1ull << Av[i];
+                  }
+#pragma unroll
+                for (int i = 0; i < NM; i++) xv[i] = XOLD(i);
+                need_scan = false;
+                need_select = true;
+              } else {
+                act |= 1ull << ip;
+                need_scan = need_select = true;
+              }
+            } else {  // partial step: drop l, refresh s[ip] = CI[:,ip]^T x + ci0[ip]
+              act &= ~(1ull << l);
+              delete_constraint(l);
+              double s = 0.0;
+#pragma unroll
+              for (int j = 0; j < NM; j++)
+                if (j < n) s += npv[j] * xv[j];
+              lput<MM>(sv, ip, s + ci0ip);
+              need_scan = need_select = false;
+            }
+          }
         }
-        need_scan = need_select = false;
       }
     }
+    if (a.stamps && lane == 0) {
+      a.stamps[(uint64_t)blockIdx.x * kStampSlots + 5] = tscan;
+      a.stamps[(uint64_t)blockIdx.x * kStampSlots + 6] = tsel;
+      a.stamps[(uint64_t)blockIdx.x * kStampSlots + 7] = nloop;
+    }
   }
-#undef JL
+#undef Jr_
+#undef XOLD
+#undef UOLD
+#undef AOLD
+  qp_stamp(a, 3);
 
-  if (write_x) {
-    double* xb = a.x + qbase<T>(b, n);
+  if (live) {
+    if (chol_ok) {
+      double* xb = view(a.x, n);
 #pragma unroll
-    for (int i = 0; i < NM; i++)
-      if (i < n) xb[i * T] = xv[i];
+      for (int i = 0; i < NM; i++)
+        if (i < n) xb[i * T] = xv[i];
+    }
+    a.f[b] = fval;
+    a.status[b] = status;
+    if (a.iters) a.iters[b] = iter;
   }
-  a.f[b] = fval;
-  a.status[b] = status;
-  if (a.iters) a.iters[b] = iter;
+  qp_stamp(a, 4);
+}
+
+template <int NM, int MM, int T>
+static void launch_lane_t(const QpArgs& a, hipStream_t stream, int64_t blocks) {
+  if (a.n == NM && a.m == MM)
+    hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, true>), dim3((unsigned)blocks), dim3(64), 0, stream, a);
+  else
+    hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, false>), dim3((unsigned)blocks), dim3(64), 0, stream, a);
 }
 
 template <int NM, int MM>
 static hipError_t launch_lane(const QpArgs& a, hipStream_t stream) {
   const int64_t blocks = (a.batch + 63) / 64;
   if (a.tile == 64)
-    hipLaunchKernelGGL((qp_lane_kernel<NM, MM, 64>), dim3((unsigned)blocks), dim3(64), 0, stream, a);
+    launch_lane_t<NM, MM, 64>(a, stream, blocks);
   else
-    hipLaunchKernelGGL((qp_lane_kernel<NM, MM, 1>), dim3((unsigned)blocks), dim3(64), 0, stream, a);
+    launch_lane_t<NM, MM, 1>(a, stream, blocks);
   return hipGetLastError();
 }
 

@@ -30,6 +30,7 @@ extern "C" hipError_t qpk_relayout(int64_t batch, int E, const double* src, doub
 namespace {
 
 thread_local std::string g_last_error;
+uint64_t* g_stamps = nullptr;  // diagnostic stamp buffer (qpgpu_debug_set_stamps)
 
 int hip_fail(hipError_t e, const char* what) {
   g_last_error = std::string(what) + ": " + hipGetErrorString(e);
@@ -127,6 +128,7 @@ int qpgpu_solve_batched(const qpgpu_problem_desc* d, double* G, const double* g0
   a.f = f;
   a.status = status;
   a.iters = iters;
+  a.stamps = g_stamps;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int handled = 0;
   hipError_t e = hipSuccess;
@@ -226,6 +228,10 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const doubl
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
   return QPGPU_SUCCESS;
 }
+
+// Diagnostic hook (not in include/qpgpu.h): device buffer of kStampSlots uint64 per wave that
+// the next launches fill with s_memtime phase stamps; NULL turns it off.
+void qpgpu_debug_set_stamps(void* dev_buf) { g_stamps = static_cast<uint64_t*>(dev_buf); }
 
 int qpgpu_relayout(int64_t batch, int32_t elems, const double* src, double* dst, int32_t to_tiled,
                    void* stream) {

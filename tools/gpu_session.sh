@@ -36,12 +36,16 @@ for s in $STEPS; do
     pmc)
       run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu
       run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu ;;
+    benchj)
+      for j in 0 1; do for l in qp_major tiled64; do QPGPU_LANE_JREG=$j run bench_jreg${j}_$l 600 python bench.py --family lane --layout $l --no-cpu; done; done ;;
+    stamps) for l in qp_major tiled64; do run stamps_general_$l 300 python tools/stamps.py general $l; run stamps_box_$l 300 python tools/stamps.py box $l; done ;;
     listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;
     sq)
       for f in ${FAMILIES:-lane subgroup}; do
-        run sqA_$f 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d "$OUT/sqA_$f" -o c1 -- python3 bench.py --steps 3 --warmup 1 --no-cpu --family $f
-        run sqB_$f 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d "$OUT/sqB_$f" -o c1 -- python3 bench.py --steps 3 --warmup 1 --no-cpu --family $f
-        run sqC_$f 600 rocprofv3 --pmc SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH --output-format csv -d "$OUT/sqC_$f" -o c1 -- python3 bench.py --steps 3 --warmup 1 --no-cpu --family $f
+        export QPGPU_LANE_JREG=${JREG:-0}
+        run sqA_$f 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d "$OUT/sqA_$f" -o c1 -- python3 bench.py --steps 3 --warmup 1 --no-cpu --family $f --layout ${LAYOUT:-qp_major}
+        run sqB_$f 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d "$OUT/sqB_$f" -o c1 -- python3 bench.py --steps 3 --warmup 1 --no-cpu --family $f --layout ${LAYOUT:-qp_major}
+        run sqC_$f 600 rocprofv3 --pmc SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH --output-format csv -d "$OUT/sqC_$f" -o c1 -- python3 bench.py --steps 3 --warmup 1 --no-cpu --family $f --layout ${LAYOUT:-qp_major}
       done ;;
   esac
 done

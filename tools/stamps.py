@@ -1,0 +1,49 @@
+"""Diagnostic: per-phase s_memtime stamps of the lane kernel (qpgpu_debug_set_stamps).
+
+Runs the bench workload once with stamps on and prints, per phase, cycles per wave
+(mean / p50 / p90 / max) plus the wave's l1-pass maximum.  Never used for timing numbers."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "motion-generation-using-quadratic-programs_amd"))
+import qpgpu  # noqa: E402
+
+kind, n, p, m = (sys.argv[1] if len(sys.argv) > 1 else "general"), 7, 6, 14
+layout = sys.argv[2] if len(sys.argv) > 2 else "qp_major"
+if kind == "box":
+    p = 0
+B = 65536
+pr = qpgpu.make_problems(kind, n, p, m, 0, B, seed=2026)
+db = qpgpu.DeviceBatch(pr, "cuda:0", layout=layout)
+waves = (B + 63) // 64
+st = torch.zeros(waves * 8, dtype=torch.int64, device="cuda:0")
+fn = qpgpu.LIB.qpgpu_debug_set_stamps
+fn.argtypes = [ctypes.c_void_p]
+for rep in range(3):
+    fn(ctypes.c_void_p(st.data_ptr()))
+    db.solve(family="lane")
+    torch.cuda.synchronize()
+fn(None)
+s = st.cpu().numpy().reshape(waves, 8).astype(np.int64)
+it = db.iters.cpu().numpy()[: waves * 64].reshape(waves, 64)
+names = ["loads+setup", "equality", "active-set", "stores"]
+tot = s[:, 4] - s[:, 0]
+print(f"{kind} {layout}: total cycles/wave mean {tot.mean():.0f} p50 {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max()}")
+for k, nm in enumerate(names):
+    d = s[:, k + 1] - s[:, k]
+    print(f"  {nm:12s} mean {d.mean():9.0f} p50 {np.median(d):9.0f} p90 {np.percentile(d, 90):9.0f} max {d.max():9d}")
+asp = s[:, 3] - s[:, 2]
+print(f"  in loop: iterations/wave mean {s[:, 7].mean():.2f} max {s[:, 7].max()}; scan {s[:, 5].mean():.0f} "
+      f"select {s[:, 6].mean():.0f} l2a+rest {(asp - s[:, 5] - s[:, 6]).mean():.0f} cycles/wave")
+mx = it.max(axis=1)
+print("  l1 passes: lane mean", it.mean(), "wave-max mean", mx.mean(), "max", mx.max())
+for v in sorted(set(mx.tolist())):
+    sel = mx == v
+    print(f"    wave-max {v}: {sel.sum():5d} waves, active-set cycles mean {(s[sel, 3] - s[sel, 2]).mean():.0f}")
+start = s[:, 0] - s[:, 0].min()
+print("  wave start offsets (cycles): p50", np.median(start), "max", start.max(), " end max", (s[:, 4] - s[:, 0].min()).max())
