@@ -36,6 +36,7 @@ CONFIGS = {
     "C2": ("box", 7, 0, 14, 65536, "C2: 65536 x (n=7, p=0, m=14) joint-limit box QPs per GPU"),
     "C3": ("general", 30, 6, 60, 65536, "C3: 65536 x (n=30, p=6, m=60) general QPs per GPU"),
     "mgqp": ("general", 14, 10, 28, 65536, "mgqp level-0 shape: 65536 x (n=14, p=10, m=28)"),
+    "C5": ("general", 256, 0, 512, 4096, "C5: 4096 x (n=256, p=0, m=512) general QPs per GPU"),
 }
 
 
@@ -47,7 +48,7 @@ def parse():
     ap.add_argument("--config", default="C1", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="QPs per GPU (default: config's)")
     ap.add_argument("--seed", type=int, default=2026)
-    ap.add_argument("--family", default=None, choices=["lane", "subgroup"],
+    ap.add_argument("--family", default=None, choices=["lane", "subgroup", "wave"],
                     help="force a kernel family (default: the dispatcher's choice)")
     ap.add_argument("--layout", default="qp_major", choices=["qp_major", "tiled64"],
                     help="batch layout of the resident inputs (include/qpgpu.h)")
@@ -103,7 +104,8 @@ def main():
     pr = qpgpu.make_problems(kind, n, p, m, rank * B, (rank + 1) * B, seed=args.seed)
     kname = qpgpu.kernel_name(n, p, m)
     if args.family:
-        kname = {"lane": f"qp_lane[n={n},m={m}]", "subgroup": f"qp_small[n={n},m={m}]"}[args.family]
+        kname = {"lane": f"qp_lane[n={n},m={m}]", "subgroup": f"qp_small[n={n},m={m}]",
+                 "wave": f"qp_wave[n={n},m={m}]"}[args.family]
     if not kname:
         sys.exit(f"no gfx950 kernel covers (n, p, m) = {(n, p, m)}")
     bufs = [qpgpu.DeviceBatch(pr, dev, with_iters=False, layout=args.layout)]

@@ -88,10 +88,14 @@ enum qpgpu_error {
 
 /* Kernel-family selection (benchmarking / testing knobs; default = fastest for the shape):
  *   LANE      one QP per lane (qp_lane.hip, n <= 8, m <= 16)
- *   SUBGROUP  one QP per S-lane subgroup (qp_small.hip, n <= 16, m <= 64)
+ *   SUBGROUP  one QP per S-lane subgroup, register state (qp_small.hip, n <= 16, m <= 64)
+ *   WAVE      one QP per 32/64/256 lanes, LDS / workspace state (qp_wave.hip, n <= 256,
+ *             m <= 1024; n > 64 uses a cached device workspace of ~1 MiB per QP, allocated by
+ *             the first call for that size — call once before capturing into a hipGraph)
  * Forcing a family that does not cover the shape returns QPGPU_ERR_UNSUPPORTED_SHAPE. */
 #define QPGPU_FLAG_FORCE_LANE 0x100u
 #define QPGPU_FLAG_FORCE_SUBGROUP 0x200u
+#define QPGPU_FLAG_FORCE_WAVE 0x400u
 
 typedef struct qpgpu_problem_desc {
   int32_t n;         /* variables                      (G.ncols() in the reference)  */

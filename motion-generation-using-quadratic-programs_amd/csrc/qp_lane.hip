@@ -59,27 +59,22 @@ constexpr int kStage = 5120;  // staging buffer, doubles (40 KiB: 4 waves per CU
 
 __device__ __forceinline__ bool wave_any(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
 
-template <int NM, int MM, int T, bool EXACT>
-__global__ void __launch_bounds__(64) qp_lane_kernel(const QpArgs a) {
+// QPW = QPs per wavefront (64, or 32 to run two waves per SIMD with half the lanes each)
+template <int NM, int MM, int T, bool EXACT, int QPW>
+__global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const QpArgs a) {
+  static_assert(QPW == 64 || (QPW == 32 && T == 1), "half waves only with the QP-major layout");
   static_assert(MM <= 64, "bitmask bookkeeping holds m <= 64");
-  static_assert(64 * (NM * NM | 1) + 64 * (NM | 1) <= kStage, "G + g0 must fit one stage");
   using RI = RIdx<NM>;
-  // scan staging: TILED64 rounds of RPR CI rows (+ ci0 in the last round); QP-major rounds
-  // of QPR whole QPs (CI + ci0 blocks)
-  constexpr int RPR = (kStage - (64 * MM + 127) / 128 * 128) / (64 * MM);
-  constexpr int NROUND = (NM + RPR - 1) / RPR;
-  static_assert(RPR >= 1, "stage buffer too small for one CI row");
-  constexpr int QPR = ((64 * (NM * MM + MM) + 127) / 128 * 128 <= kStage) ? 64 : 32;
-  static_assert((QPR * NM * MM + 127) / 128 * 128 + QPR * MM <= kStage, "CI half-tile must fit");
   // LDS per wave: J region + rollback region (40 KiB at NM = 7: 4 waves/CU)
-  constexpr int STAGE_MIN = (64 * NM * NM + 127) / 128 * 128 + 64 * (3 * NM + 2);
-  constexpr int STAGE = STAGE_MIN > kStage ? STAGE_MIN : kStage;
+  constexpr int STAGE_MIN = (QPW * NM * NM + 127) / 128 * 128 + QPW * (3 * NM + 2);
+  constexpr int STAGE_CAP = kStage * QPW / 64;
+  constexpr int STAGE = STAGE_MIN > STAGE_CAP ? STAGE_MIN : STAGE_CAP;
   __shared__ double sbuf[STAGE];
 
   const int lane = threadIdx.x;
-  const int64_t b0 = (int64_t)blockIdx.x * 64;
+  const int64_t b0 = (int64_t)blockIdx.x * QPW;
   const int64_t b = b0 + lane;
-  const int valid = (int)min<int64_t>(64, a.batch - b0);
+  const int valid = (int)min<int64_t>(QPW, a.batch - b0);
   const bool live = lane < valid;
 
   // EXACT: the shape is (NM, *, MM), so every element offset is a compile-time constant
@@ -92,7 +87,7 @@ __global__ void __launch_bounds__(64) qp_lane_kernel(const QpArgs a) {
   // whole tiles, so its waves are always full).  Staging copies a contiguous span of that
   // range into sbuf with LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave-instruction, no
   // VGPRs, everything in flight at once); a partial last QP-major wave copies per lane.
-  const bool full = (T == 64) || (valid == 64);
+  const bool full = (T == 64) || (valid == QPW);
   auto copy_span = [&](const double* src, int nd, int off) {  // nd even, full waves only
 #pragma unroll 4
     for (int k = 0; k < nd; k += 128) {
@@ -105,7 +100,7 @@ __global__ void __launch_bounds__(64) qp_lane_kernel(const QpArgs a) {
   // whole tile of X (E doubles per QP) -> sbuf[off...]
   auto stage_all = [&](const double* X, int E, int off) {
     if (full) {
-      copy_span(X + b0 * (int64_t)E, 64 * E, off);
+      copy_span(X + b0 * (int64_t)E, QPW * E, off);
     } else if (live) {
       const double* src = X + b * (int64_t)E;
       for (int e = 0; e < E; e++) sbuf[off + lane * E + e] = src[e];
@@ -135,16 +130,16 @@ __global__ void __launch_bounds__(64) qp_lane_kernel(const QpArgs a) {
   // which first serves as the staging area for G and then CE; RB = g0 staging, then the
   // rollback copies x_old / u_old / A_old.  Keeping J and the rollback state out of VGPRs
   // leaves the compiler room to keep memory operations in flight.
-  constexpr int JA = (64 * NM * NM + 127) / 128 * 128;
+  constexpr int JA = (QPW * NM * NM + 127) / 128 * 128;
   constexpr int RB = JA;
-  constexpr int RB_U = RB + 64 * NM, RB_A = RB_U + 64 * (NM + 1);
-  static_assert(RB_A + 64 * (NM + 1) <= STAGE, "LDS regions exceed the stage buffer");
-#define Jr_(i, j) sbuf[((i) * NM + (j)) * 64 + lane]
+  constexpr int RB_U = RB + QPW * NM, RB_A = RB_U + QPW * (NM + 1);
+  static_assert(RB_A + QPW * (NM + 1) <= STAGE, "LDS regions exceed the stage buffer");
+#define Jr_(i, j) sbuf[((i) * NM + (j)) * QPW + lane]
   double CEr[NM][NM], ce0r[NM];  // CEr[i][j] = CE[j][i] (column i = equality constraint i)
   qp_stamp(a, 0);
 
   // ---------------------------------------------------------------- setup
-  bool chol_ok = true;
+  bool chol_ok = live;  // idle lanes (past the batch, or lanes >= QPW) never touch LDS slots
   double bad_sum = 0.0;
   {
     double Gr[NM][NM];
@@ -157,15 +152,15 @@ __global__ void __launch_bounds__(64) qp_lane_kernel(const QpArgs a) {
 #pragma unroll
     for (int i = 0; i < NM; i++) {
 #pragma unroll
-      for (int j = 0; j < NM; j++) Gr[i][j] = (i < n && j < n) ? rd_all(0, n * n, i * n + j) : 0.0;
-      g0v[i] = (i < n) ? rd_all(offg0, n, i) : 0.0;
+      for (int j = 0; j < NM; j++) Gr[i][j] = (live && i < n && j < n) ? rd_all(0, n * n, i * n + j) : 0.0;
+      g0v[i] = (live && i < n) ? rd_all(offg0, n, i) : 0.0;
     }
     __syncthreads();
     // round B: CE and ce0 (equality phase), issued now so they land during the Cholesky
     if (p > 0) {
       const int np_ = n * p;
-      const int offc = (64 * np_ + 127) / 128 * 128;
-      if (offc + 64 * p <= STAGE) {
+      const int offc = (QPW * np_ + 127) / 128 * 128;
+      if (offc + QPW * p <= STAGE) {
         stage_all(a.CE, np_, 0);
         stage_all(a.ce0, p, offc);
       }
@@ -210,8 +205,8 @@ __global__ void __launch_bounds__(64) qp_lane_kernel(const QpArgs a) {
     // round B lands: CE columns into registers (before J overwrites the JA region)
     if (p > 0) {
       const int np_ = n * p;
-      const int offc = (64 * np_ + 127) / 128 * 128;
-      const bool staged = offc + 64 * p <= STAGE;
+      const int offc = (QPW * np_ + 127) / 128 * 128;
+      const bool staged = offc + QPW * p <= STAGE;
       __syncthreads();
   #pragma unroll
       for (int i = 0; i < NM; i++) {
@@ -532,9 +527,9 @@ __global__ void __launch_bounds__(64) qp_lane_kernel(const QpArgs a) {
     double sv[MM];
 #pragma unroll
     for (int i = 0; i < MM; i++) sv[i] = 0.0;
-#define XOLD(i) sbuf[RB + (i) * 64 + lane]
-#define UOLD(i) sbuf[RB_U + (i) * 64 + lane]
-#define AOLD(i) sbuf[RB_A + (i) * 64 + lane]
+#define XOLD(i) sbuf[RB + (i) * QPW + lane]
+#define UOLD(i) sbuf[RB_U + (i) * QPW + lane]
+#define AOLD(i) sbuf[RB_A + (i) * QPW + lane]
     uint64_t act = 0;   // bit c set <=> iai[c] == -1
     uint64_t excl = 0;  // bit c set <=> iaexcl[c] == false
     int ip = 0, steps = 0;
@@ -787,21 +782,36 @@ __global__ void __launch_bounds__(64) qp_lane_kernel(const QpArgs a) {
   qp_stamp(a, 4);
 }
 
-template <int NM, int MM, int T>
-static void launch_lane_t(const QpArgs& a, hipStream_t stream, int64_t blocks) {
+template <int NM, int MM, int T, int QPW>
+static void launch_lane_t(const QpArgs& a, hipStream_t stream) {
+  const int64_t blocks = (a.batch + QPW - 1) / QPW;
   if (a.n == NM && a.m == MM)
-    hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, true>), dim3((unsigned)blocks), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, true, QPW>), dim3((unsigned)blocks), dim3(64), 0,
+                       stream, a);
   else
-    hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, false>), dim3((unsigned)blocks), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, false, QPW>), dim3((unsigned)blocks), dim3(64), 0,
+                       stream, a);
+}
+
+// QPs per wave for the QP-major layout: QPGPU_LANE_QPW=32 runs half-filled waves at two waves
+// per SIMD (tuning knob; default 64).
+static int lane_qpw() {
+  static int v = 0;
+  if (!v) {
+    const char* e = getenv("QPGPU_LANE_QPW");
+    v = (e && atoi(e) == 32) ? 32 : 64;
+  }
+  return v;
 }
 
 template <int NM, int MM>
 static hipError_t launch_lane(const QpArgs& a, hipStream_t stream) {
-  const int64_t blocks = (a.batch + 63) / 64;
   if (a.tile == 64)
-    launch_lane_t<NM, MM, 64>(a, stream, blocks);
+    launch_lane_t<NM, MM, 64, 64>(a, stream);
+  else if (lane_qpw() == 32)
+    launch_lane_t<NM, MM, 1, 32>(a, stream);
   else
-    launch_lane_t<NM, MM, 1>(a, stream, blocks);
+    launch_lane_t<NM, MM, 1, 64>(a, stream);
   return hipGetLastError();
 }
 

@@ -1,0 +1,710 @@
+// qp_wave.hip — gfx950 batched Goldfarb–Idnani solver for larger dense QPs (16 < n <= 256).
+//
+// Restates solve_quadprog() (reference include/QuadProgpp/QuadProg++.hh:69-72; operation order
+// of the prebuilt libquadprog.a fixed in SURVEY.md §3.2).  One QP per SUBGROUP of S lanes
+// (S = 32: two QPs per wavefront; S = 64: one; S = 256: a 4-wave workgroup), split as:
+//   * "lead" work — the O(n) / O(iq^2) serial chains (Givens coefficients, update_r, step
+//     lengths, dot products, active-set bookkeeping) — runs on lane 0 of every subgroup, so a
+//     wave advances 64/S QPs' serial chains with each instruction;
+//   * row-/column-parallel work — compute_d (lane = column of J), update_z and every Givens
+//     row update (lane = row of J), the l1 scan s = CI^T x + ci0 (lane = constraint, CI rows
+//     read coalesced from HBM/L2), the Cholesky column, the J = L^{-T} rows — is spread over
+//     the subgroup's lanes.  Every parallel element keeps the reference's summation order, so
+//     results are bitwise identical to the CPU restatement (oracle/qp_oracle.c).
+// State lives in LDS (per QP: J and R [n][n+1], vectors, bookkeeping) with dynamic indexing;
+// with GJR, J and R live in a global workspace instead (n = 256: 2 x 514 KiB per QP).  The
+// lead lane exchanges scalars with its subgroup through an LDS control block.
+#include "qp_common.h"
+
+namespace qpk {
+
+template <int S>
+__device__ __forceinline__ void grp_sync() {
+  if constexpr (S > 64)
+    __syncthreads();
+  else
+    sg_sync();
+}
+
+// per-QP control block (lead lane writes, subgroup reads after grp_sync)
+struct Ctl {
+  double f, t, t1, t2, ss, R_norm, c1, c2, psi, ci0ip, znp;
+  int iq, ip, l, status, phase, iter, steps, flags, qq, ngiv, fin;
+  int pad[5];
+};
+
+enum : int {
+  PH_DONE = 0,
+  PH_SCAN = 1,   // l1
+  PH_SELECT = 2, // l2
+  PH_STEP = 3    // l2a
+};
+
+template <int S, int NMAX, int MMAX, bool GJR>
+struct WaveCfg {
+  static constexpr int QPB = S >= 64 ? 1 : 64 / S;  // QPs per block
+  static constexpr int BS = S >= 64 ? S : 64;       // threads per block
+  static constexpr int JS = NMAX + 1;               // row stride of J and R
+  // LDS doubles per QP
+  static constexpr int OFF_J = 0;
+  static constexpr int OFF_R = GJR ? 0 : OFF_J + NMAX * JS;
+  static constexpr int OFF_V = GJR ? 0 : OFF_R + NMAX * JS;
+  static constexpr int OFF_X = OFF_V, OFF_Z = OFF_X + NMAX, OFF_D = OFF_Z + NMAX, OFF_NP = OFF_D + NMAX;
+  static constexpr int OFF_RR = OFF_NP + NMAX, OFF_XO = OFF_RR + NMAX;
+  static constexpr int OFF_GC = OFF_XO + NMAX, OFF_GS = OFF_GC + NMAX, OFF_GX = OFF_GS + NMAX;
+  static constexpr int OFF_GF = OFF_GX + NMAX;  // Givens step applied (1.0) / skipped (0.0)
+  static constexpr int OFF_U = OFF_GF + NMAX, OFF_UO = OFF_U + NMAX + 1;
+  static constexpr int OFF_S = OFF_UO + NMAX + 1;
+  static constexpr int OFF_A = OFF_S + MMAX;                        // int[NMAX+1] x 2
+  static constexpr int OFF_FL = OFF_A + (2 * (NMAX + 1) + 1) / 2;  // uint8[MMAX] x 2
+  static constexpr int OFF_CTL = OFF_FL + (2 * MMAX + 7) / 8;
+  static constexpr int PER_QP = OFF_CTL + (int)(sizeof(Ctl) / 8);
+  static constexpr int STRIDE = PER_QP | 1;
+  static constexpr int LDS_DOUBLES = QPB * STRIDE;
+  static constexpr int WS_DOUBLES = GJR ? 2 * NMAX * JS : 0;  // per QP, global workspace
+};
+
+template <int S, int NMAX, int MMAX, bool GJR>
+__global__ void __launch_bounds__(S >= 64 ? S : 64)
+    qp_wave_kernel(const QpArgs a, double* __restrict__ ws) {
+  using C = WaveCfg<S, NMAX, MMAX, GJR>;
+  constexpr int JS = C::JS;
+  __shared__ double lds[C::LDS_DOUBLES];
+
+  const int tid = threadIdx.x;
+  const int sg = S >= 64 ? 0 : tid / S;
+  const int ls = S >= 64 ? tid : tid - sg * S;
+  const bool lead = (ls == 0);
+  const int64_t b = (int64_t)blockIdx.x * C::QPB + sg;
+  const bool live = b < a.batch;  // whole subgroups only
+
+  double* const Q = lds + sg * C::STRIDE;
+  double* const Jm = GJR ? ws + (b < a.batch ? b : 0) * (int64_t)C::WS_DOUBLES : Q + C::OFF_J;
+  double* const Rm = GJR ? Jm + NMAX * JS : Q + C::OFF_R;
+  double* const xv = Q + C::OFF_X;
+  double* const zv = Q + C::OFF_Z;
+  double* const dv = Q + C::OFF_D;
+  double* const npv = Q + C::OFF_NP;
+  double* const rv = Q + C::OFF_RR;
+  double* const xo = Q + C::OFF_XO;
+  double* const gc = Q + C::OFF_GC;
+  double* const gs = Q + C::OFF_GS;
+  double* const gx = Q + C::OFF_GX;
+  double* const gf = Q + C::OFF_GF;
+  double* const uv = Q + C::OFF_U;
+  double* const uo = Q + C::OFF_UO;
+  double* const sv = Q + C::OFF_S;
+  int* const Av = reinterpret_cast<int*>(Q + C::OFF_A);
+  int* const Ao = Av + NMAX + 1;
+  uint8_t* const act = reinterpret_cast<uint8_t*>(Q + C::OFF_FL);  // iai[i] == -1
+  uint8_t* const exc = act + MMAX;                                  // !iaexcl[i]
+  Ctl* const ctl = reinterpret_cast<Ctl*>(Q + C::OFF_CTL);
+
+  const int n = a.n, p = a.p, m = a.m, T = a.tile;
+  const double inf = dinf();
+  const int64_t bb = live ? b : 0;
+  const double* Gb = a.G + qbase_rt(bb, n * n, T);
+  const double* g0b = a.g0 + qbase_rt(bb, n, T);
+  const double* CEb = a.CE + qbase_rt(bb, n * p, T);
+  const double* ce0b = a.ce0 + qbase_rt(bb, p, T);
+  const double* CIb = a.CI + qbase_rt(bb, n * m, T);
+  const double* ci0b = a.ci0 + qbase_rt(bb, m, T);
+#define EL(ptr, e) (ptr)[(int64_t)(e) * T]
+#define J_(i, j) Jm[(i) * JS + (j)]
+#define R_(i, j) Rm[(i) * JS + (j)]
+
+  // ------------------------------------------------------------------ setup
+  // G -> R region (becomes L), g0 -> z region
+  if (live) {
+    for (int e = ls; e < n * n; e += S) {
+      const int i = e / n, j = e - (e / n) * n;
+      R_(i, j) = EL(Gb, e);
+    }
+    for (int i = ls; i < n; i += S) zv[i] = EL(g0b, i);
+  }
+  if (lead) {
+    ctl->status = QPGPU_QP_OK;
+    ctl->iter = 0;
+    ctl->steps = 0;
+    ctl->phase = live ? PH_SCAN : PH_DONE;
+    ctl->fin = 1;
+  }
+  grp_sync<S>();
+  if (live) {
+    if (lead) {
+      double c1 = 0.0;
+      for (int i = 0; i < n; i++) c1 += R_(i, i);
+      ctl->c1 = c1;
+    }
+    // cholesky_decomposition (@.text+0x2df0): row-wise, descending-k sums, upper mirrored.
+    for (int i = 0; i < n; i++) {
+      if (lead) {
+        double sum = R_(i, i);
+        for (int k = i - 1; k >= 0; k--) sum -= R_(i, k) * R_(i, k);
+        if (sum <= 0.0) {
+          ctl->status = QPGPU_QP_NOT_POSITIVE_DEFINITE;
+          ctl->f = sum;
+        } else {
+          ctl->t = sqrt(sum);  // the pivot, shared with the subgroup
+        }
+      }
+      grp_sync<S>();
+      if (ctl->status != QPGPU_QP_OK) break;
+      const double dg = ctl->t;
+      for (int j = i + 1 + ls; j < n; j += S) {
+        double s2 = R_(i, j);
+        for (int k = i - 1; k >= 0; k--) s2 -= R_(i, k) * R_(j, k);
+        R_(j, i) = s2 / dg;
+      }
+      if (lead) R_(i, i) = dg;
+      grp_sync<S>();
+      for (int k = i + 1 + ls; k < n; k += S) R_(i, k) = R_(k, i);
+      grp_sync<S>();
+    }
+  }
+  const bool chol_ok = live && ctl->status == QPGPU_QP_OK;
+  if (live && (a.flags & QPGPU_FLAG_WRITE_FACTOR)) {
+    double* Gw = a.G + qbase_rt(bb, n * n, T);
+    for (int e = ls; e < n * n; e += S) EL(Gw, e) = R_(e / n, e - (e / n) * n);
+  }
+  if (chol_ok) {
+    // J = L^{-T}: lane r builds row r = (L^{-1} e_r)^T in place (J_(r, .) is its own scratch).
+    // With a finite L the first r entries are exactly +0.0 and add exact zeros later: skipped
+    // (same bits).  A non-finite L takes the literal path.
+    if (lead) {
+      int fin = 1;
+      for (int i = 0; i < n && fin; i++)
+        for (int j = 0; j <= i; j++)
+          if (!(fabs(R_(i, j)) < inf)) {
+            fin = 0;
+            break;
+          }
+      ctl->fin = fin;
+    }
+    grp_sync<S>();
+    const bool skip = ctl->fin != 0;
+    for (int r = ls; r < n; r += S) {
+      const int i0 = skip ? r : 0;
+      for (int i = 0; i < i0; i++) J_(r, i) = 0.0;
+      for (int i = i0; i < n; i++) {
+        double v = (i == r) ? 1.0 : 0.0;
+        for (int j = i0; j < i; j++) v -= R_(i, j) * J_(r, j);
+        J_(r, i) = v / R_(i, i);
+      }
+    }
+    grp_sync<S>();
+    if (lead) {
+      double c2 = 0.0;
+      for (int i = 0; i < n; i++) c2 += J_(i, i);
+      ctl->c2 = c2;
+      // cholesky_solve (@.text+0x31a2): y -> d, x = -G^{-1} g0
+      for (int i = 0; i < n; i++) {
+        double v = zv[i];
+        for (int j = 0; j < i; j++) v -= R_(i, j) * dv[j];
+        dv[i] = v / R_(i, i);
+      }
+      for (int i = n - 1; i >= 0; i--) {
+        double v = dv[i];
+        for (int j = i + 1; j < n; j++) v -= R_(i, j) * xv[j];
+        xv[i] = v / R_(i, i);
+      }
+      double f = 0.0;
+      for (int i = 0; i < n; i++) {
+        xv[i] = -xv[i];
+        f += zv[i] * xv[i];
+      }
+      ctl->f = 0.5 * f;
+      ctl->R_norm = 1.0;
+      ctl->iq = 0;
+    }
+    grp_sync<S>();
+    // R = 0 (L no longer needed), flags
+    for (int e = ls; e < n * JS; e += S) Rm[e] = 0.0;
+    for (int i = ls; i < m; i += S) act[i] = exc[i] = 0;
+    for (int i = ls; i <= n; i += S) {
+      uv[i] = 0.0;
+      Av[i] = 0;
+    }
+    grp_sync<S>();
+  }
+
+  // ------------------------------------------------------------------ shared kernels
+  // d = J^T np (lane = column, j ascending); z = J[:, iq:] d[iq:] (lane = row)
+  auto compute_d_z = [&](int iq) {
+    for (int c = ls; c < n; c += S) {
+      double s = 0.0;
+      for (int j = 0; j < n; j++) s += J_(j, c) * npv[j];
+      dv[c] = s;
+    }
+    grp_sync<S>();
+    for (int r = ls; r < n; r += S) {
+      double z = 0.0;
+      for (int j = iq; j < n; j++) z += J_(r, j) * dv[j];
+      zv[r] = z;
+    }
+    grp_sync<S>();
+  };
+  // lead: update_r (r = R[:iq,:iq]^{-1} d[:iq])
+  auto update_r_lead = [&](int iq) {
+    for (int i = iq - 1; i >= 0; i--) {
+      double s = 0.0;
+      for (int j = i + 1; j < iq; j++) s += R_(i, j) * rv[j];
+      rv[i] = (dv[i] - s) / R_(i, i);
+    }
+  };
+  auto dot_lead = [&](const double* u_, const double* v_) {
+    double s = 0.0;
+    for (int i = 0; i < n; i++) s += u_[i] * v_[i];
+    return s;
+  };
+  // add_constraint (@.text+0x21fd), split: the lead runs the d-chain and records each Givens
+  // coefficient set (gc, gs, gx; gx = NaN marks a skipped |h| < eps step), every lane then
+  // applies the recorded rotations to its rows of J in the same order; the lead finishes with
+  // R[:iq, iq-1] = d and the degeneracy test.  Returns through ctl->fin (1 = added).
+  // gf[g] = 0 marks a step the reference skips (|h| < eps).
+  auto add_constraint = [&]() {
+    if (lead) {
+      const int iq = ctl->iq;
+      int ng = 0;
+      if (iq < n) {
+        for (int j = n - 1; j >= iq + 1; j--) {
+          double cc = dv[j - 1], ss = dv[j];
+          const double h = qp_distance(cc, ss);
+          if (fabs(h) < kEps) {
+            gf[ng++] = 0.0;
+            continue;
+          }
+          dv[j] = 0.0;
+          ss = ss / h;
+          cc = cc / h;
+          if (cc < 0.0) {
+            cc = -cc;
+            ss = -ss;
+            dv[j - 1] = -h;
+          } else {
+            dv[j - 1] = h;
+          }
+          gc[ng] = cc;
+          gs[ng] = ss;
+          gx[ng] = ss / (1.0 + cc);
+          gf[ng++] = 1.0;
+        }
+      }
+      ctl->ngiv = ng;
+    }
+    grp_sync<S>();
+    const int iq0 = ctl->iq;
+    if (iq0 < n) {
+      const int ng = ctl->ngiv;
+      for (int k = ls; k < n; k += S) {
+        for (int g = 0; g < ng; g++) {
+          if (gf[g] == 0.0) continue;  // skipped step
+          const double xny = gx[g];
+          const int j = n - 1 - g;
+          const double cc = gc[g], ss = gs[g];
+          const double t1 = J_(k, j - 1), t2 = J_(k, j);
+          const double n1 = t1 * cc + t2 * ss;
+          J_(k, j - 1) = n1;
+          J_(k, j) = xny * (t1 + n1) - t2;
+        }
+      }
+    }
+    grp_sync<S>();
+    if (lead) {
+      int iq = ctl->iq;
+      if (iq >= n) {
+        ctl->fin = 0;  // reference UB (p > n); reported as dependent
+      } else {
+        iq++;
+        for (int i = 0; i < iq; i++) R_(i, iq - 1) = dv[i];
+        ctl->iq = iq;
+        const double dd = fabs(dv[iq - 1]);
+        if (dd <= kEps * ctl->R_norm) {
+          ctl->fin = 0;
+        } else {
+          ctl->R_norm = (ctl->R_norm < dd) ? dd : ctl->R_norm;
+          ctl->fin = 1;
+        }
+      }
+    }
+    grp_sync<S>();
+  };
+  // delete_constraint (@.text+0x26a8) of constraint l: the lead does the bookkeeping and the
+  // R re-triangularisation (recording the rotations), the lanes shift R's rows and rotate
+  // J's columns.
+  auto delete_constraint = [&](int l) {
+    if (lead) {
+      const int iq = ctl->iq;
+      int qq = 0;
+      for (int i = p; i < iq; i++)
+        if (Av[i] == l) {
+          qq = i;
+          break;
+        }
+      for (int i = qq; i < iq - 1; i++) {
+        Av[i] = Av[i + 1];
+        uv[i] = uv[i + 1];
+      }
+      Av[iq - 1] = Av[iq];
+      uv[iq - 1] = uv[iq];
+      Av[iq] = 0;
+      uv[iq] = 0.0;
+      ctl->qq = qq;
+    }
+    grp_sync<S>();
+    {
+      const int iq = ctl->iq, qq = ctl->qq;
+      for (int j = ls; j < n; j += S) {
+        for (int i = qq; i < iq - 1; i++) R_(j, i) = R_(j, i + 1);
+        if (j < iq) R_(j, iq - 1) = 0.0;
+      }
+    }
+    grp_sync<S>();
+    if (lead) {
+      const int iq = --ctl->iq;
+      const int qq = ctl->qq;
+      int ng = 0;
+      if (iq > 0) {
+        for (int j = qq; j < iq; j++) {
+          double cc = R_(j, j), ss = R_(j + 1, j);
+          const double h = qp_distance(cc, ss);
+          if (fabs(h) < kEps) {
+            gf[ng++] = 0.0;
+            continue;
+          }
+          cc = cc / h;
+          ss = ss / h;
+          R_(j + 1, j) = 0.0;
+          if (cc < 0.0) {
+            R_(j, j) = -h;
+            cc = -cc;
+            ss = -ss;
+          } else {
+            R_(j, j) = h;
+          }
+          const double xny = ss / (1.0 + cc);
+          for (int k = j + 1; k < iq; k++) {
+            const double t1 = R_(j, k), t2 = R_(j + 1, k);
+            const double r1 = t1 * cc + t2 * ss;
+            R_(j, k) = r1;
+            R_(j + 1, k) = xny * (t1 + r1) - t2;
+          }
+          gc[ng] = cc;
+          gs[ng] = ss;
+          gx[ng] = xny;
+          gf[ng++] = 1.0;
+        }
+      }
+      ctl->ngiv = ng;
+    }
+    grp_sync<S>();
+    {
+      const int ng = ctl->ngiv, qq = ctl->qq;
+      for (int k = ls; k < n; k += S) {
+        for (int g = 0; g < ng; g++) {
+          if (gf[g] == 0.0) continue;
+          const double xny = gx[g];
+          const int j = qq + g;
+          const double cc = gc[g], ss = gs[g];
+          const double t1 = J_(k, j), t2 = J_(k, j + 1);
+          const double n1 = t1 * cc + t2 * ss;
+          J_(k, j) = n1;
+          J_(k, j + 1) = xny * (n1 + t1) - t2;
+        }
+      }
+    }
+    grp_sync<S>();
+  };
+
+  // ------------------------------------------------------------------ equality phase
+  if (chol_ok) {
+    for (int i = 0; i < p; i++) {
+      for (int j = ls; j < n; j += S) npv[j] = EL(CEb, j * p + i);
+      grp_sync<S>();
+      compute_d_z(ctl->iq);
+      if (lead) {
+        const int iq = ctl->iq;
+        update_r_lead(iq);
+        double t2 = 0.0;
+        const double zz = dot_lead(zv, zv);
+        const double znp = dot_lead(zv, npv);
+        if (fabs(zz) > kEps) t2 = (-dot_lead(npv, xv) - EL(ce0b, i)) / znp;
+        ctl->t2 = t2;
+        uv[iq] = t2;
+        for (int k = 0; k < iq; k++) uv[k] -= t2 * rv[k];
+        ctl->f += 0.5 * (t2 * t2) * znp;
+        Av[i] = -i - 1;
+      }
+      grp_sync<S>();
+      {
+        const double t2 = ctl->t2;
+        for (int k = ls; k < n; k += S) xv[k] += t2 * zv[k];
+      }
+      add_constraint();
+      if (!ctl->fin) {
+        if (lead) {
+          ctl->status = QPGPU_QP_DEPENDENT;
+          ctl->phase = PH_DONE;
+        }
+        grp_sync<S>();
+        break;
+      }
+    }
+  } else if (lead) {
+    ctl->phase = PH_DONE;
+  }
+  grp_sync<S>();
+
+  // ------------------------------------------------------------------ active-set loop
+  // Per-subgroup state machine; a wave loops until all of its QPs are done.
+  const int max_steps = a.max_steps;
+  while (true) {
+    const int phase = ctl->phase;
+    if (S < 64) {
+      if (__builtin_amdgcn_ballot_w64(phase != PH_DONE) == 0) break;
+    } else if (phase == PH_DONE) {
+      break;
+    }
+    if (phase == PH_DONE) continue;  // other subgroups of this wave are still busy
+    if (phase == PH_SCAN) {
+      // ---- l1
+      if (lead) {
+        ctl->iter++;
+        for (int i = p; i < ctl->iq; i++) act[Av[i]] = 1;
+      }
+      for (int i = ls; i < m; i += S) {
+        double s = 0.0;
+        for (int j = 0; j < n; j++) s += EL(CIb, j * m + i) * xv[j];
+        s += EL(ci0b, i);
+        sv[i] = s;
+        exc[i] = 0;
+      }
+      grp_sync<S>();
+      if (lead) {
+        double psi = 0.0;
+        for (int i = 0; i < m; i++) psi += (sv[i] < 0.0) ? sv[i] : 0.0;
+        ctl->ss = 0.0;
+        ctl->ip = 0;
+        if (fabs(psi) <= (double)m * kEps * ctl->c1 * ctl->c2 * 100.0) {
+          ctl->phase = PH_DONE;
+        } else {
+          for (int i = 0; i < ctl->iq; i++) {
+            uo[i] = uv[i];
+            Ao[i] = Av[i];
+          }
+          ctl->phase = PH_SELECT;
+        }
+      }
+      for (int i = ls; i < n; i += S) xo[i] = xv[i];
+      grp_sync<S>();
+      continue;
+    }
+    if (phase == PH_SELECT) {
+      // ---- l2 (ss deliberately not reset: reference quirk)
+      if (lead) {
+        double ss = ctl->ss;
+        int ip = ctl->ip;
+        for (int i = 0; i < m; i++)
+          if (sv[i] < ss && !act[i] && !exc[i]) {
+            ss = sv[i];
+            ip = i;
+          }
+        ctl->ss = ss;
+        ctl->ip = ip;
+        if (ss >= 0.0) {
+          ctl->phase = PH_DONE;
+        } else {
+          uv[ctl->iq] = 0.0;
+          Av[ctl->iq] = ip;
+          ctl->ci0ip = EL(ci0b, ip);
+          ctl->phase = PH_STEP;
+        }
+      }
+      grp_sync<S>();
+      if (ctl->phase == PH_STEP) {
+        const int ip = ctl->ip;
+        for (int j = ls; j < n; j += S) npv[j] = EL(CIb, j * m + ip);
+        grp_sync<S>();
+      }
+      continue;
+    }
+    // ---- l2a (phase == PH_STEP)
+    if (lead) {
+      if (max_steps > 0 && ++ctl->steps > max_steps) {
+        ctl->status = QPGPU_QP_MAX_ITER;
+        ctl->phase = PH_DONE;
+      }
+    }
+    grp_sync<S>();
+    if (ctl->phase == PH_DONE) continue;
+    compute_d_z(ctl->iq);
+    int kind = 0;  // 1 infeasible, 2 dual step, 3 full step, 4 partial step
+    if (lead) {
+      const int iq = ctl->iq;
+      update_r_lead(iq);
+      int l = 0;
+      double t1 = inf;
+      for (int k = p; k < iq; k++)
+        if (rv[k] > 0.0 && uv[k] / rv[k] < t1) {
+          t1 = uv[k] / rv[k];
+          l = Av[k];
+        }
+      double t2;
+      const double zz = dot_lead(zv, zv);
+      const double znp = dot_lead(zv, npv);
+      if (fabs(zz) > kEps) {
+        t2 = -sv[ctl->ip] / znp;
+        if (t2 < 0) t2 = inf;  // Takano Akio patch
+      } else {
+        t2 = inf;
+      }
+      const double t = (t2 < t1) ? t2 : t1;
+      ctl->t = t;
+      ctl->t1 = t1;
+      ctl->t2 = t2;
+      ctl->l = l;
+      if (t >= inf) {
+        ctl->status = QPGPU_QP_INFEASIBLE;
+        ctl->f = inf;
+        ctl->phase = PH_DONE;
+        kind = 1;
+      } else if (t2 >= inf) {
+        for (int k = 0; k < iq; k++) uv[k] -= t * rv[k];
+        uv[iq] += t;
+        act[l] = 0;
+        kind = 2;
+      } else {
+        ctl->f += t * znp * (0.5 * t + uv[iq]);
+        for (int k = 0; k < iq; k++) uv[k] -= t * rv[k];
+        uv[iq] += t;
+        kind = (fabs(t - t2) < kEps) ? 3 : 4;
+      }
+      ctl->qq = kind;  // broadcast the branch
+    }
+    grp_sync<S>();
+    kind = ctl->qq;
+    if (kind == 1) continue;
+    if (kind == 2) {
+      delete_constraint(ctl->l);
+      if (lead) ctl->phase = PH_STEP;
+      grp_sync<S>();
+      continue;
+    }
+    {
+      const double t = ctl->t;
+      for (int k = ls; k < n; k += S) xv[k] += t * zv[k];
+    }
+    grp_sync<S>();
+    if (kind == 3) {
+      add_constraint();
+      if (!ctl->fin) {
+        const int ip = ctl->ip;
+        if (lead) exc[ip] = 1;
+        grp_sync<S>();
+        delete_constraint(ip);
+        if (lead) {
+          for (int i = 0; i < m; i++) act[i] = 0;
+          for (int i = p; i < ctl->iq; i++) {
+            Av[i] = Ao[i];
+            uv[i] = uo[i];
+            act[Av[i]] = 1;
+          }
+          ctl->phase = PH_SELECT;
+        }
+        for (int i = ls; i < n; i += S) xv[i] = xo[i];
+      } else {
+        if (lead) {
+          act[ctl->ip] = 1;
+          ctl->phase = PH_SCAN;
+        }
+      }
+      grp_sync<S>();
+      continue;
+    }
+    // partial step: drop l, refresh s[ip]
+    if (lead) act[ctl->l] = 0;
+    grp_sync<S>();
+    delete_constraint(ctl->l);
+    if (lead) {
+      double s = 0.0;
+      for (int k = 0; k < n; k++) s += npv[k] * xv[k];
+      sv[ctl->ip] = s + ctl->ci0ip;
+      ctl->phase = PH_STEP;
+    }
+    grp_sync<S>();
+  }
+#undef J_
+#undef R_
+
+  // ------------------------------------------------------------------ outputs
+  if (live) {
+    const int st = ctl->status;
+    if (st != QPGPU_QP_NOT_POSITIVE_DEFINITE) {
+      double* xb = a.x + qbase_rt(bb, n, T);
+      for (int i = ls; i < n; i += S) EL(xb, i) = xv[i];
+    }
+    if (lead) {
+      a.f[b] = ctl->f;
+      a.status[b] = st;
+      if (a.iters) a.iters[b] = ctl->iter;
+    }
+  }
+#undef EL
+}
+
+// ------------------------------------------------------------------------------------------
+template <int S, int NMAX, int MMAX, bool GJR>
+static hipError_t launch_wave(const QpArgs& a, hipStream_t stream, double* ws) {
+  using C = WaveCfg<S, NMAX, MMAX, GJR>;
+  const int64_t blocks = (a.batch + C::QPB - 1) / C::QPB;
+  hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR>), dim3((unsigned)blocks), dim3(C::BS), 0,
+                     stream, a, ws);
+  return hipGetLastError();
+}
+
+struct WaveVariant {
+  int nmax, mmax;
+  int64_t ws_doubles_per_qp;
+  const char* name;
+  hipError_t (*launch)(const QpArgs&, hipStream_t, double*);
+};
+
+static const WaveVariant kWaveVariants[] = {
+    {32, 64, 0, "qp_wave<S=32,N=32,M=64>", launch_wave<32, 32, 64, false>},
+    {32, 128, 0, "qp_wave<S=32,N=32,M=128>", launch_wave<32, 32, 128, false>},
+    {64, 128, 0, "qp_wave<S=64,N=64,M=128>", launch_wave<64, 64, 128, false>},
+    {64, 256, 0, "qp_wave<S=64,N=64,M=256>", launch_wave<64, 64, 256, false>},
+    {256, 1024, WaveCfg<256, 256, 1024, true>::WS_DOUBLES, "qp_wave<S=256,N=256,M=1024,global J/R>",
+     launch_wave<256, 256, 1024, true>},
+};
+
+const WaveVariant* pick_wave(int n, int m) {
+  for (const auto& v : kWaveVariants)
+    if (n <= v.nmax && m <= v.mmax) return &v;
+  return nullptr;
+}
+
+}  // namespace qpk
+
+extern "C" const char* qpk_medium_name(int n, int /*p*/, int m) {
+  const qpk::WaveVariant* v = qpk::pick_wave(n, m);
+  return v ? v->name : nullptr;
+}
+extern "C" int qpk_medium_max_n(void) { return 256; }
+extern "C" int qpk_medium_max_m(void) { return 1024; }
+// bytes of device workspace the medium kernels need for a batch (0 = none)
+extern "C" int64_t qpk_medium_workspace_bytes(int n, int m, int64_t batch) {
+  const qpk::WaveVariant* v = qpk::pick_wave(n, m);
+  return v ? v->ws_doubles_per_qp * 8 * batch : 0;
+}
+extern "C" hipError_t qpk_launch_medium_ws(const qpk::QpArgs* a, hipStream_t stream, int* handled,
+                                          const char** name, double* ws) {
+  const qpk::WaveVariant* v = qpk::pick_wave(a->n, a->m);
+  if (!v) {
+    *handled = 0;
+    return hipSuccess;
+  }
+  *handled = 1;
+  if (name) *name = v->name;
+  return v->launch(*a, stream, ws);
+}

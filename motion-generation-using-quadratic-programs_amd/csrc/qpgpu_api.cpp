@@ -19,8 +19,9 @@ extern "C" const char* qpk_small_name(int n, int p, int m);
 extern "C" hipError_t qpk_launch_lane(const qpk::QpArgs* a, hipStream_t stream, int* handled,
                                       const char** name);
 extern "C" const char* qpk_lane_name(int n, int p, int m);
-extern "C" hipError_t qpk_launch_medium(const qpk::QpArgs* a, hipStream_t stream, int* handled,
-                                        const char** name);
+extern "C" hipError_t qpk_launch_medium_ws(const qpk::QpArgs* a, hipStream_t stream, int* handled,
+                                           const char** name, double* ws);
+extern "C" int64_t qpk_medium_workspace_bytes(int n, int m, int64_t batch);
 extern "C" const char* qpk_medium_name(int n, int p, int m);
 extern "C" int qpk_medium_max_n(void);
 extern "C" int qpk_medium_max_m(void);
@@ -47,10 +48,11 @@ int validate(const qpgpu_problem_desc* d) {
   if (d->n <= 0 || d->p < 0 || d->m < 0 || d->batch < 0) return QPGPU_ERR_INVALID_ARGUMENT;
   if (d->layout != QPGPU_LAYOUT_QP_MAJOR && d->layout != QPGPU_LAYOUT_TILED64)
     return QPGPU_ERR_INVALID_ARGUMENT;
-  const uint32_t known = QPGPU_FLAG_WRITE_FACTOR | QPGPU_FLAG_FORCE_LANE | QPGPU_FLAG_FORCE_SUBGROUP;
+  const uint32_t fam = QPGPU_FLAG_FORCE_LANE | QPGPU_FLAG_FORCE_SUBGROUP | QPGPU_FLAG_FORCE_WAVE;
+  const uint32_t known = QPGPU_FLAG_WRITE_FACTOR | fam;
   if (d->flags & ~known) return QPGPU_ERR_INVALID_ARGUMENT;
-  if ((d->flags & QPGPU_FLAG_FORCE_LANE) && (d->flags & QPGPU_FLAG_FORCE_SUBGROUP))
-    return QPGPU_ERR_INVALID_ARGUMENT;
+  const uint32_t f = d->flags & fam;
+  if (f & (f - 1)) return QPGPU_ERR_INVALID_ARGUMENT;  // at most one family
   return QPGPU_SUCCESS;
 }
 
@@ -65,6 +67,39 @@ struct HostWorkspace {
   }
 };
 thread_local HostWorkspace g_ws;
+
+// Device workspace for the kernels that keep J and R in global memory (n > 64).  Grow-only,
+// one per device, shared by all threads (serialised by a mutex; kernels on different streams
+// must not overlap on it — documented in include/qpgpu.h).
+struct DevWorkspace {
+  void* buf = nullptr;
+  size_t bytes = 0;
+};
+std::mutex g_dev_ws_mu;
+DevWorkspace g_dev_ws[64];
+
+int device_workspace(int64_t bytes, double** out) {
+  *out = nullptr;
+  if (bytes <= 0) return QPGPU_SUCCESS;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  if (dev < 0 || dev >= 64) return QPGPU_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(g_dev_ws_mu);
+  DevWorkspace& w = g_dev_ws[dev];
+  if (w.bytes < (size_t)bytes) {
+    if (w.buf) {
+      if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+      (void)hipFree(w.buf);
+      w.buf = nullptr;
+      w.bytes = 0;
+    }
+    if ((e = hipMalloc(&w.buf, (size_t)bytes)) != hipSuccess) return hip_fail(e, "hipMalloc workspace");
+    w.bytes = (size_t)bytes;
+  }
+  *out = static_cast<double*>(w.buf);
+  return QPGPU_SUCCESS;
+}
 
 }  // namespace
 
@@ -133,15 +168,26 @@ int qpgpu_solve_batched(const qpgpu_problem_desc* d, double* G, const double* g0
   int handled = 0;
   hipError_t e = hipSuccess;
   a.flags = d->flags & QPGPU_FLAG_WRITE_FACTOR;
+  auto launch_wave = [&]() -> int {
+    double* ws = nullptr;
+    const int wrc = device_workspace(qpk_medium_workspace_bytes(a.n, a.m, a.batch), &ws);
+    if (wrc) return wrc;
+    e = qpk_launch_medium_ws(&a, s, &handled, nullptr, ws);
+    return QPGPU_SUCCESS;
+  };
+  int wrc = QPGPU_SUCCESS;
   if (d->flags & QPGPU_FLAG_FORCE_LANE) {
     e = qpk_launch_lane(&a, s, &handled, nullptr);
   } else if (d->flags & QPGPU_FLAG_FORCE_SUBGROUP) {
     e = qpk_launch_small(&a, s, &handled, nullptr);
+  } else if (d->flags & QPGPU_FLAG_FORCE_WAVE) {
+    wrc = launch_wave();
   } else {
     e = qpk_launch_lane(&a, s, &handled, nullptr);
     if (!handled) e = qpk_launch_small(&a, s, &handled, nullptr);
-    if (!handled) e = qpk_launch_medium(&a, s, &handled, nullptr);
+    if (!handled) wrc = launch_wave();
   }
+  if (wrc) return wrc;
   if (!handled) return QPGPU_ERR_UNSUPPORTED_SHAPE;
   if (e != hipSuccess) return hip_fail(e, "kernel launch");
   return QPGPU_SUCCESS;

@@ -46,7 +46,9 @@ ERR_NO_DEVICE = 4
 FLAG_WRITE_FACTOR = 0x1
 FLAG_FORCE_LANE = 0x100
 FLAG_FORCE_SUBGROUP = 0x200
-FAMILY_FLAGS = {None: 0, "auto": 0, "lane": FLAG_FORCE_LANE, "subgroup": FLAG_FORCE_SUBGROUP}
+FLAG_FORCE_WAVE = 0x400
+FAMILY_FLAGS = {None: 0, "auto": 0, "lane": FLAG_FORCE_LANE, "subgroup": FLAG_FORCE_SUBGROUP,
+                "wave": FLAG_FORCE_WAVE}
 LAYOUT_QP_MAJOR = 0
 LAYOUT_TILED64 = 1
 LAYOUTS = {None: 0, "qp_major": LAYOUT_QP_MAJOR, "tiled64": LAYOUT_TILED64}

@@ -21,6 +21,20 @@ CONFIGS = [
 ]
 
 
+# shapes only the qp_wave kernels cover (n > 16), with batch sizes the oracle finishes quickly
+LARGE_CONFIGS = [
+    ("n17_general", "general", 17, 3, 40, 256),
+    ("n32_general", "general", 32, 8, 64, 256),
+    ("n33_box", "box", 33, 0, 66, 128),
+    ("n48_general", "general", 48, 10, 100, 64),
+    ("n64_general", "general", 64, 0, 128, 32),
+    ("n64_box", "box", 64, 0, 128, 32),
+    ("n100_general", "general", 100, 20, 200, 8),
+    ("C5_n256_box", "box", 256, 0, 512, 4),
+    ("C5_n256_general", "general", 256, 0, 512, 2),
+]
+
+
 def make(kind, n, p, m, B, seed=12345):
     return qpgpu.make_problems(kind, n, p, m, 0, B, seed=seed)
 

@@ -29,7 +29,7 @@ def _relerr(a, b):
     return float(np.max(r)) if r.size else 0.0
 
 
-FAMILIES = (None, "lane", "subgroup")
+FAMILIES = (None, "lane", "subgroup", "wave")
 
 
 def covers(family, n, m):
@@ -37,6 +37,8 @@ def covers(family, n, m):
         return n <= 8 and m <= 16
     if family == "subgroup":
         return n <= 16 and m <= 64
+    if family == "wave":
+        return n <= 256 and m <= 1024
     return bool(qpgpu.kernel_name(n, 0, m))
 
 
@@ -84,6 +86,11 @@ def test_config_parity(gpu, name, kind, n, p, m, family):
 @pytest.mark.parametrize("name,pr", qp_cases.edge_cases(), ids=[c[0] for c in qp_cases.edge_cases()])
 def test_edge_parity(gpu, name, pr, family, layout):
     assert_parity(pr, name, write_factor=True, family=family, layout=layout)
+
+
+@pytest.mark.parametrize("name,kind,n,p,m,B", qp_cases.LARGE_CONFIGS)
+def test_large_config_parity(gpu, name, kind, n, p, m, B):
+    assert_parity(qp_cases.make(kind, n, p, m, B, seed=11), name)
 
 
 @pytest.mark.parametrize("family", FAMILIES)

@@ -31,7 +31,8 @@ for s in $STEPS; do
     benchfam)
       for f in ${FAMILIES:-lane subgroup}; do for l in qp_major tiled64; do run bench_${f}_$l 600 python bench.py --family $f --layout $l --no-cpu; done; done ;;
     benchall)
-      for c in C1 C2 mgqp; do run bench_$c 600 python bench.py --config $c --no-cpu; done ;;
+      for c in C1 C2 mgqp C3; do run bench_$c 600 python bench.py --config $c --no-cpu; done
+      run bench_C5 600 python bench.py --config C5 --no-cpu --steps 3 --warmup 1 ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c1 -- python3 bench.py --steps 20 --warmup 5 --no-cpu ;;
     pmc)
       run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu
@@ -39,6 +40,8 @@ for s in $STEPS; do
     benchj)
       for j in 0 1; do for l in qp_major tiled64; do QPGPU_LANE_JREG=$j run bench_jreg${j}_$l 600 python bench.py --family lane --layout $l --no-cpu; done; done ;;
     stamps) for l in qp_major tiled64; do run stamps_general_$l 300 python tools/stamps.py general $l; run stamps_box_$l 300 python tools/stamps.py box $l; done ;;
+    benchqpw)
+      for q in 64 32; do QPGPU_LANE_QPW=$q run bench_qpw$q 600 python bench.py --family lane --no-cpu; done ;;
     listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;
     sq)
       for f in ${FAMILIES:-lane subgroup}; do
