@@ -26,6 +26,7 @@ sys.path.insert(0, os.path.join(ROOT, "motion-generation-using-quadratic-program
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+import qpdist  # noqa: E402
 import qpgpu  # noqa: E402
 
 METRIC = "QP solves/sec at n=7,p=6,m=14 batch=65536; achieved HBM GB/s vs peak"
@@ -91,17 +92,23 @@ def main():
         if world == 1 and args.gpus > 1:
             sys.exit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
     dist = None
+    # one rank per GPU; "nccl" is RCCL on ROCm.  QPGPU_DIST_BACKEND=gloo rehearses the N>1 flow
+    # with several ranks on one GPU (results then travel through host memory).
+    backend = os.environ.get("QPGPU_DIST_BACKEND", "nccl")
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     kind, n, p, m, bdef, desc = CONFIGS[args.config]
     B = args.batch or bdef
-    pr = qpgpu.make_problems(kind, n, p, m, rank * B, (rank + 1) * B, seed=args.seed)
+    b0, b1 = qpdist.shard(rank, B)
+    pr = qpgpu.make_problems(kind, n, p, m, b0, b1, seed=args.seed)
     kname = qpgpu.kernel_name(n, p, m)
     if args.family:
         kname = {"lane": f"qp_lane[n={n},m={m}]", "subgroup": f"qp_small[n={n},m={m}]",
@@ -118,8 +125,9 @@ def main():
         b2.status = torch.empty_like(bufs[0].status)
         bufs.append(b2)
         rows = bufs[0].x.shape[0]
-        packed = [torch.empty((rows, n + 2), dtype=torch.float64, device=dev) for _ in range(2)]
-        recv = [torch.empty((rows, n + 2), dtype=torch.float64, device=dev) for _ in range(world)] if rank == 0 else None
+        pdev = dev if backend == "nccl" else torch.device("cpu")
+        packed = [torch.empty((rows, n + 2), dtype=torch.float64, device=pdev) for _ in range(2)]
+        recv = [torch.empty((rows, n + 2), dtype=torch.float64, device=pdev) for _ in range(world)] if rank == 0 else None
         comm = torch.cuda.Stream(dev)
         works = [None, None]
     compute = torch.cuda.current_stream(dev)
@@ -135,14 +143,18 @@ def main():
         if ev:
             ev[1].record(compute)
         if gather:
+            # pack (x, f, status) and gather to rank 0 on the comm stream, overlapping the next
+            # step's solve (double-buffered outputs)
             pk = packed[k % 2]
-            pk[:, :n].copy_(db.x)
-            pk[:B, n].copy_(db.f)
-            pk[:B, n + 1].copy_(db.status.to(torch.float64))
-            done = torch.cuda.Event()
-            done.record(compute)
-            with torch.cuda.stream(comm):
-                comm.wait_event(done)
+            if backend == "nccl":
+                pk.copy_(qpdist.pack_results(db.x, db.f, db.status))
+                done = torch.cuda.Event()
+                done.record(compute)
+                with torch.cuda.stream(comm):
+                    comm.wait_event(done)
+                    works[k % 2] = dist.gather(pk, recv if rank == 0 else None, dst=0, async_op=True)
+            else:
+                pk.copy_(qpdist.pack_results(db.x, db.f, db.status).cpu())
                 works[k % 2] = dist.gather(pk, recv if rank == 0 else None, dst=0, async_op=True)
 
     for k in range(args.warmup):

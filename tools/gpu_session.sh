@@ -36,12 +36,14 @@ for s in $STEPS; do
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c1 -- python3 bench.py --steps 20 --warmup 5 --no-cpu ;;
     pmc)
       run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu
-      run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu ;;
+      run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu
+      python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" C1 65536 "$(python3 -c 'import sys; sys.path.insert(0,"motion-generation-using-quadratic-programs_amd"); import qpgpu; print(qpgpu.kernel_name(7,6,14))')" "$OUT/pmc_traffic.json" ;;
     benchj)
       for j in 0 1; do for l in qp_major tiled64; do QPGPU_LANE_JREG=$j run bench_jreg${j}_$l 600 python bench.py --family lane --layout $l --no-cpu; done; done ;;
     stamps) for l in qp_major tiled64; do run stamps_general_$l 300 python tools/stamps.py general $l; run stamps_box_$l 300 python tools/stamps.py box $l; done ;;
     benchqpw)
       for q in 64 32; do QPGPU_LANE_QPW=$q run bench_qpw$q 600 python bench.py --family lane --no-cpu; done ;;
+    dist2) QPGPU_DIST_BACKEND=gloo run dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 ;;
     listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;
     sq)
       for f in ${FAMILIES:-lane subgroup}; do
