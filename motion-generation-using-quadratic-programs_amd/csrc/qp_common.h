@@ -74,6 +74,8 @@ struct QpArgs {
   uint64_t* stamps;
 };
 constexpr int kStampSlots = 8;
+// internal QpArgs.flags bit set by the host when CI and ci0 are 16-byte aligned
+constexpr uint32_t kArgAligned16 = 0x80000000u;
 
 __device__ __forceinline__ void qp_stamp(const QpArgs& a, int slot) {
   if (a.stamps) {

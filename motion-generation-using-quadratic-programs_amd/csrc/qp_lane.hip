@@ -60,7 +60,9 @@ constexpr int kStage = 5120;  // staging buffer, doubles (40 KiB: 4 waves per CU
 __device__ __forceinline__ bool wave_any(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
 
 // QPW = QPs per wavefront (64, or 32 to run two waves per SIMD with half the lanes each)
-template <int NM, int MM, int T, bool EXACT, int QPW>
+// PX >= 0: p is the compile-time constant PX as well (C1/C4: 6, C2: 0), which folds every
+// [p, iq) loop of the active-set phase (for n = 7, p = 6 that range holds at most one entry).
+template <int NM, int MM, int T, bool EXACT, int QPW, int PX>
 __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const QpArgs a) {
   static_assert(QPW == 64 || (QPW == 32 && T == 1), "half waves only with the QP-major layout");
   static_assert(MM <= 64, "bitmask bookkeeping holds m <= 64");
@@ -80,7 +82,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   // EXACT: the shape is (NM, *, MM), so every element offset is a compile-time constant
   const int n = EXACT ? NM : a.n;
   const int m = EXACT ? MM : a.m;
-  const int p = a.p;
+  const int p = PX >= 0 ? PX : a.p;
   const double inf = dinf();
 
   // The wave's 64 QPs occupy [X + b0*E, X + (b0+64)*E) in both layouts (TILED64 arrays hold
@@ -592,17 +594,45 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
         // of the scheduler's one-load-at-a-time minimum-pressure order.
         if (do_scan) {
           double rowbuf[2][MM];
+          // QP-major rows of an EXACT even-m shape are 16-B aligned when the arrays are
+          // (checked on the host: kArgAligned16): load them as dwordx4, half the instructions
+          // and half the cache-line lookups per row
+          constexpr bool VEC = (T == 1) && EXACT && (MM % 2 == 0);
+          const bool vec = VEC && (a.flags & kArgAligned16);
+          auto ldrow = [&](double* dst, const double* src) {
+            if (VEC && vec) {
 #pragma unroll
-          for (int i = 0; i < MM; i++) rowbuf[0][i] = (i < m) ? ldCI(i) : 0.0;
+              for (int i = 0; i < MM; i += 2) {
+                const double2 v = *reinterpret_cast<const double2*>(src + i);
+                dst[i] = v.x;
+                dst[i + 1] = v.y;
+              }
+            } else {
+#pragma unroll
+              for (int i = 0; i < MM; i++) dst[i] = (i < m) ? src[i] : 0.0;
+            }
+          };
+          if constexpr (T == 1)
+            ldrow(rowbuf[0], CIg);
+          else
+#pragma unroll
+            for (int i = 0; i < MM; i++) rowbuf[0][i] = (i < m) ? ldCI(i) : 0.0;
 #pragma unroll
           for (int j = 0; j < NM; j++) {
             if (j + 1 < NM) {
+              if constexpr (T == 1) {
+                if (j + 1 < n) ldrow(rowbuf[(j + 1) & 1], CIg + (j + 1) * m);
+              } else {
 #pragma unroll
-              for (int i = 0; i < MM; i++)
-                rowbuf[(j + 1) & 1][i] = (j + 1 < n && i < m) ? ldCI((j + 1) * m + i) : 0.0;
+                for (int i = 0; i < MM; i++)
+                  rowbuf[(j + 1) & 1][i] = (j + 1 < n && i < m) ? ldCI((j + 1) * m + i) : 0.0;
+              }
             } else {
+              if constexpr (T == 1)
+                ldrow(rowbuf[(j + 1) & 1], ci0g);
+              else
 #pragma unroll
-              for (int i = 0; i < MM; i++) rowbuf[(j + 1) & 1][i] = (i < m) ? ldci0(i) : 0.0;
+                for (int i = 0; i < MM; i++) rowbuf[(j + 1) & 1][i] = (i < m) ? ldci0(i) : 0.0;
             }
             __builtin_amdgcn_sched_barrier(0);
             if (j < n) {
@@ -785,12 +815,17 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
 template <int NM, int MM, int T, int QPW>
 static void launch_lane_t(const QpArgs& a, hipStream_t stream) {
   const int64_t blocks = (a.batch + QPW - 1) / QPW;
-  if (a.n == NM && a.m == MM)
-    hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, true, QPW>), dim3((unsigned)blocks), dim3(64), 0,
-                       stream, a);
-  else
-    hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, false, QPW>), dim3((unsigned)blocks), dim3(64), 0,
-                       stream, a);
+  const dim3 g((unsigned)blocks), blk(64);
+  if (a.n == NM && a.m == MM) {
+    if (QPW == 64 && a.p == 6)
+      hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, true, QPW, 6>), g, blk, 0, stream, a);
+    else if (QPW == 64 && a.p == 0)
+      hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, true, QPW, 0>), g, blk, 0, stream, a);
+    else
+      hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, true, QPW, -1>), g, blk, 0, stream, a);
+  } else {
+    hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, false, QPW, -1>), g, blk, 0, stream, a);
+  }
 }
 
 // QPs per wave for the QP-major layout: QPGPU_LANE_QPW=32 runs half-filled waves at two waves

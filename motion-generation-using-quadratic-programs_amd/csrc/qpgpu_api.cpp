@@ -168,6 +168,8 @@ int qpgpu_solve_batched(const qpgpu_problem_desc* d, double* G, const double* g0
   int handled = 0;
   hipError_t e = hipSuccess;
   a.flags = d->flags & QPGPU_FLAG_WRITE_FACTOR;
+  if (((reinterpret_cast<uintptr_t>(CI) | reinterpret_cast<uintptr_t>(ci0)) & 15u) == 0)
+    a.flags |= qpk::kArgAligned16;
   auto launch_wave = [&]() -> int {
     double* ws = nullptr;
     const int wrc = device_workspace(qpk_medium_workspace_bytes(a.n, a.m, a.batch), &ws);
