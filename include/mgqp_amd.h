@@ -1,0 +1,95 @@
+/* mgqp_amd.h — C-ABI of the motion-generation controller.
+ *
+ * Wraps mgqp_amd::MotionGenerationQuadraticProgram (include/quadprog_amd/mgqp.hh) for FFI
+ * callers (ctypes in tests/ and bench.py).  Every entry replaces one member of the reference
+ * component:
+ *   mgqp_set_dof              <- setDOFsize            (reference src/mgqp.cpp:180)
+ *   mgqp_set_gains            <- setGains              (src/mgqp.cpp:1208)
+ *   mgqp_set_torque_limits    <- setTorqueLimits       (src/mgqp.cpp:494)
+ *   mgqp_set_acceleration_limits <- setAccelerationLimits (src/mgqp.cpp:503)
+ *   mgqp_set_angular_limits   <- setAngularLimits      (src/mgqp.cpp:512)
+ *   mgqp_set_priority_level   <- setPriorityLevel      (src/mgqp.cpp:560)
+ *   mgqp_update               <- updateHook            (src/mgqp.cpp:872-1189)
+ *   mgqp_update_batched       <- updateHook for `count` robots in one pass (GPU batched solves)
+ *   mgqp_nullspace_projector  <- the JacobiSVD null-space block (src/mgqp.cpp:836-862)
+ * Input ports are pointers; NULL stands for RTT::NoData.  All matrices are row-major float.
+ */
+#ifndef MGQP_AMD_H
+#define MGQP_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mgqp_ctl mgqp_ctl;
+
+typedef struct {
+  const float* desired_ts_position;     /* in_desiredTaskSpacePosition_port_j   (ts_len) */
+  const float* desired_ts_velocity;     /* in_desiredTaskSpaceVelocity_port_j */
+  const float* desired_ts_acceleration; /* in_desiredTaskSpaceAcceleration_port_j */
+  const float* current_ts_position;     /* in_currentTaskSpacePosition_port_j */
+  const float* current_ts_velocity;     /* in_currentTaskSpaceVelocity_port_j */
+  const float* current_ts_acceleration; /* in_currentTaskSpaceAcceleration_port_j */
+  const float* desired_js_position;     /* in_desiredJointSpacePosition_port_j   (scalar) */
+  const float* desired_js_velocity;     /* in_desiredJointSpaceVelocity_port_j */
+  const float* desired_js_acceleration; /* in_desiredJointSpaceAcceleration_port_j */
+  const float* jacobian;                /* in_jacobian_port_j     (jac_rows x jac_cols) */
+  const float* jacobian_dot;            /* in_jacobianDot_port_j  (jac_rows x jac_cols) */
+  int32_t ts_len;
+  int32_t jac_rows;
+  int32_t jac_cols;
+  int32_t reserved;
+} mgqp_joint_ports;
+
+typedef struct {
+  const float* angles;            /* in_robotstatus_port: angles (status_len) */
+  const float* velocities;        /*                      velocities (status_len) */
+  const float* h;                 /* in_h_port (DOF) */
+  const float* inertia;           /* in_inertia_port (DOF x DOF) */
+  const mgqp_joint_ports* joints; /* DOF entries; joint j <-> port suffix j+1 */
+  int32_t status_len;
+  int32_t reserved;
+} mgqp_cycle_inputs;
+
+/* updateHook exit codes */
+enum {
+  MGQP_CYCLE_WRITTEN = 0,     /* output ports written */
+  MGQP_CYCLE_NO_DATA = 1,     /* "FAILED, NO DATA, RETURN" */
+  MGQP_CYCLE_NO_JACOBIAN = 2, /* "FAILED, NO JACOBIAN FOR JOINT j RETURN" */
+  MGQP_CYCLE_EXCEPTION = 3    /* the reference would throw (message in mgqp_last_error) */
+};
+
+mgqp_ctl* mgqp_create(void);
+void mgqp_destroy(mgqp_ctl* c);
+void mgqp_set_dof(mgqp_ctl* c, uint32_t dof);
+void mgqp_set_gains(mgqp_ctl* c, float kp, float kd);
+int mgqp_set_torque_limits(mgqp_ctl* c, const double* P, const double* N, int32_t count);
+int mgqp_set_acceleration_limits(mgqp_ctl* c, const double* P, const double* N, int32_t count);
+int mgqp_set_angular_limits(mgqp_ctl* c, const double* sup, const double* inf, int32_t count);
+int mgqp_set_priority_level(mgqp_ctl* c, const char* task, int32_t level);
+
+/* One cycle.  torques: DOF floats (out_torques); tracking: 2*DOF floats (solveNextHierarchy
+ * result) or NULL; limits_out: 10*DOF floats (the ten out_joint*Limit* ports in declaration
+ * order PosInf, PosSup, VelInf, VelSup, AccInf, AccSup, AccDynInf, AccDynSup, TorqueInf,
+ * TorqueSup; entries of unset limits are NaN) or NULL.  Returns an MGQP_CYCLE_* code. */
+int mgqp_update(mgqp_ctl* c, const mgqp_cycle_inputs* in, float* torques, float* tracking,
+                float* limits_out);
+
+/* `count` robots sharing this controller's configuration: torques count x DOF, tracking
+ * count x 2*DOF (or NULL), codes count.  threads <= 0 picks min(16, cores).  Returns 0, or -1
+ * when a GPU call failed (mgqp_last_error). */
+int mgqp_update_batched(mgqp_ctl* c, int64_t count, const mgqp_cycle_inputs* in, float* torques,
+                        float* tracking, int32_t* codes, int32_t threads);
+
+/* Z = I - V A V^T for Acumul (rows x cols), written as dim x dim. */
+void mgqp_nullspace_projector(const float* A, int32_t rows, int32_t cols, int32_t dim, float* Z);
+
+const char* mgqp_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,169 @@
+"""Controller parity on the GPU (SURVEY.md §8(a) rows a12 solveNextStep, a13 solveNextHierarchy +
+updateHook builder).
+
+libmgqp_amd (C++ builder + hierarchy, every QP on the gfx950 kernels) against the numpy/C oracle
+restatement (oracle/mgqp_oracle.py).  The QP solves are bitwise QuadProg++ on both sides; the
+float glue around them (Eigen products and JacobiSVD in the reference) is parity unpinned, so
+outputs are compared with float tolerances: 1e-4 x max(1, |output|) (measured: <= 3e-7).  Robots
+whose hierarchy hits a numerically dependent level (a solve with |f| > 1e8, where the dual step
+blows up and the answer depends on the last float bits — chaotic in the reference too) are
+excluded and counted; they must stay rare.  The batched path must equal the single-cycle path
+bit for bit (same host arithmetic, bitwise solver).
+
+Every check takes the controller library as a parameter: test_mgqp_host.py runs the same checks
+in the CPU suite against tests/_build/libmgqp_cpu_harness.so (controller sources + the CPU oracle
+solver, test-only), this file runs them against the shipped GPU library.
+"""
+import numpy as np
+import pytest
+
+import mgqp
+import mgqp_oracle as mo
+
+pytestmark = pytest.mark.gpu
+
+LIB = None  # None = the shipped libmgqp_amd.so (GPU)
+
+
+def _wide(c=None, o=None):
+    sup = [20.0] * 7
+    if c is not None:
+        c.setAngularLimits(sup, [-s for s in sup])
+        c.setGains(10, 2)
+    if o is not None:
+        o.sup = np.full(7, 20, np.float32)
+        o.inf = -o.sup
+        o.kTP, o.kTD = np.float32(10), np.float32(2)
+
+
+def _close(a, b):
+    scale = max(1.0, float(np.abs(b).max()))
+    np.testing.assert_allclose(a, b, rtol=0, atol=1e-4 * scale)
+
+
+def _ctl(lib=None):
+    return mgqp.ops_controller(library=lib)
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_update_hook_matches_oracle(gpu, wide, lib=LIB):
+    sc = mgqp.make_scenario(48, seed=5)
+    c, o = _ctl(lib), mo.ops_oracle()
+    if wide:
+        _wide(c, o)
+    ill = 0
+    for r in range(sc.count):
+        code, tq, tr, lim = c.updateHook(sc.robot(r))
+        ocode, otq, otr = o.update(sc, r)
+        assert code == ocode == 0
+        if o.ill_conditioned:
+            ill += 1
+            continue
+        _close(tr, otr)
+        _close(tq, otq)
+        # out_jointAccDynLimitSup keeps the reference defect (src/mgqp.cpp:1161)
+        np.testing.assert_array_equal(lim["jointAccDynLimitSup"], np.full(7, 5, np.float32))
+        np.testing.assert_array_equal(lim["jointTorqueLimitInf"], np.full(7, -100, np.float32))
+    assert ill <= sc.count // 20
+
+
+def test_batched_equals_single_bitwise(gpu, lib=LIB):
+    sc = mgqp.make_scenario(96, seed=7)
+    c = _ctl(lib)
+    codes, tq, tr = c.update_batched(sc)
+    assert (codes == 0).all()
+    c1 = _ctl(lib)
+    for r in range(0, sc.count, 7):
+        code, t1, r1, _ = c1.updateHook(sc.robot(r))
+        assert code == 0
+        np.testing.assert_array_equal(tr[r], r1)
+        np.testing.assert_array_equal(tq[r], t1)
+
+
+def test_batched_wide_mixed_feasibility(gpu, lib=LIB):
+    """Wide angle limits: some robots' level-0 QPs are feasible, others need the retry without
+    inequalities (src/mgqp.cpp:717-736) — one batch holds both kinds."""
+    sc = mgqp.make_scenario(256, seed=9)
+    c, o = _ctl(lib), mo.ops_oracle()
+    _wide(c, o)
+    codes, tq, tr = c.update_batched(sc)
+    assert (codes == 0).all()
+    ill = 0
+    for r in range(0, sc.count, 4):
+        _, otq, otr = o.update(sc, r)
+        if o.ill_conditioned:
+            ill += 1
+            continue
+        _close(tr[r], otr)
+        _close(tq[r], otq)
+    assert ill <= 4
+
+
+def test_joint_beyond_limit_nan_log(gpu, lib=LIB):
+    """A joint at/over its angle limit makes log() -inf/NaN in the limits (reference defect,
+    SURVEY.md appendix A.1); std::min/std::max keep the configured limit for NaN."""
+    sc = mgqp.make_scenario(4, seed=13)
+    sc.angles[0, 0] = 0.8   # exactly at the sup limit -> log(0) = -inf
+    sc.angles[1, 2] = 2.7   # beyond the sup limit    -> log(<0) = NaN
+    sc.angles[2, 4] = -3.5  # beyond the inf limit
+    c, o = _ctl(lib), mo.ops_oracle()
+    codes, tq, tr = c.update_batched(sc)
+    for r in range(3):
+        code, otq, otr = o.update(sc, r)
+        assert codes[r] == code == 0
+        if not o.ill_conditioned:
+            _close(tr[r], otr)
+
+
+def test_early_exits(gpu, lib=LIB):
+    c = _ctl(lib)
+    sc = mgqp.make_scenario(3, seed=2)
+    sc.h = None
+    codes, _, _ = c.update_batched(sc)
+    assert (codes == mgqp.CYCLE_NO_DATA).all()
+    assert c.updateHook(sc.robot(0))[0] == mgqp.CYCLE_NO_DATA
+    sc = mgqp.make_scenario(3, seed=2)
+    del sc.ports[(6, "jacobian_dot")]
+    codes, _, _ = c.update_batched(sc)
+    assert (codes == mgqp.CYCLE_NO_JACOBIAN).all()
+    assert c.updateHook(sc.robot(1))[0] == mgqp.CYCLE_NO_JACOBIAN
+    assert "NO JACOBIAN FOR JOINT 7" in c.last_error()
+
+
+def test_dependent_equalities_raise(gpu, lib=LIB):
+    """A zero Jacobian row makes a level-0 equality row zero, so QuadProg++'s add_constraint finds
+    it dependent and solve_quadprog throws "Constraints are linearly dependent"; the C-ABI
+    reports CYCLE_EXCEPTION for that robot only."""
+    sc = mgqp.make_scenario(4, seed=21)
+    J = sc.ports[(6, "jacobian")]
+    J[1, 1] = 0
+    c, o = _ctl(lib), mo.ops_oracle()
+    codes, tq, tr = c.update_batched(sc)
+    assert codes[1] == mgqp.CYCLE_EXCEPTION and (np.delete(codes, 1) == 0).all()
+    assert c.updateHook(sc.robot(1))[0] == mgqp.CYCLE_EXCEPTION
+    assert "linearly dependent" in c.last_error()
+    with pytest.raises(RuntimeError, match="linearly dependent"):
+        o.update(sc, 1)
+
+
+def test_joint_space_levels(gpu, lib=LIB):
+    """Joint-space velocity and acceleration ports at levels 1 and 2 (builder branches at
+    src/mgqp.cpp:1006-1026): level 1 gets its own QP (pb2 at src/mgqp.cpp:789)."""
+    sc = mgqp.make_scenario(16, seed=31)
+    K = sc.count
+    sc.ports[(2, "desired_js_velocity")] = np.linspace(-0.3, 0.3, K).astype(np.float32)
+    sc.ports[(3, "desired_js_acceleration")] = np.linspace(-1, 1, K).astype(np.float32)
+    c, o = _ctl(lib), mo.ops_oracle()
+    for ctl in (c, o):
+        for name, lvl in (("in_desiredJointSpaceVelocity_3", 1),
+                          ("in_desiredJointSpaceAcceleration_4", 2)):
+            if ctl is c:
+                assert c.setPriorityLevel(name, lvl)
+            else:
+                o.levels[name] = lvl
+    codes, tq, tr = c.update_batched(sc)
+    for r in range(K):
+        code, otq, otr = o.update(sc, r)
+        assert codes[r] == code == 0
+        if not o.ill_conditioned:
+            _close(tr[r], otr)
