@@ -130,7 +130,7 @@ def build_harness():
                            os.path.join(root, "oracle", "qp_oracle.c"), "-o", obj,
                            "-I" + os.path.join(root, "include")])
     subprocess.check_call(["g++", "-O2", "-fPIC", "-std=c++17", "-ffp-contract=off", "-shared",
-                           "-pthread", "-I" + os.path.join(root, "include"),
+                           "-pthread", "-Wl,-Bsymbolic", "-I" + os.path.join(root, "include"),
                            "-I" + os.path.join(root, "include", "quadprog_amd"), "-o", HARNESS,
                            os.path.join(root, "tests", "mgqp_cpu_harness.cpp"),
                            os.path.join(pkg, "mgqp_controller.cpp"),
