@@ -83,6 +83,36 @@ int mgqp_update(mgqp_ctl* c, const mgqp_cycle_inputs* in, float* torques, float*
 int mgqp_update_batched(mgqp_ctl* c, int64_t count, const mgqp_cycle_inputs* in, float* torques,
                         float* tracking, int32_t* codes, int32_t threads);
 
+/* Device-resident batch: every pointer is DEVICE memory, robot-major
+ * (robot r's block at r * block size).  NULL = RTT::NoData for all robots of the batch. */
+#define MGQP_MAX_DOF 16
+typedef struct {
+  int64_t count;
+  const float* angles;      /* [count][status_len] */
+  const float* velocities;  /* [count][status_len] */
+  const float* h;           /* [count][DOF] */
+  const float* inertia;     /* [count][DOF][DOF] */
+  const float* ts[MGQP_MAX_DOF][6]; /* joint j: desired pos/vel/acc, current pos/vel/acc [count][ts_len[j]] */
+  const float* js[MGQP_MAX_DOF][3]; /* joint j: desired joint pos/vel/acc [count] */
+  const float* jacobian[MGQP_MAX_DOF];     /* [count][jac_rows[j]][jac_cols[j]] */
+  const float* jacobian_dot[MGQP_MAX_DOF];
+  int32_t ts_len[MGQP_MAX_DOF];
+  int32_t jac_rows[MGQP_MAX_DOF];
+  int32_t jac_cols[MGQP_MAX_DOF];
+  int32_t status_len;
+  int32_t reserved;
+} mgqp_device_batch;
+
+/* One control cycle for `b->count` robots entirely on the GPU: builder, per-level QPs, the
+ * batched solver (with the reference's retry without inequalities), null-space projector and
+ * outputs, enqueued on `stream` (hipStream_t; NULL = default).  torques [count][DOF],
+ * tracking [count][2*DOF] (or NULL), codes [count] are DEVICE arrays; codes get
+ * MGQP_CYCLE_WRITTEN or MGQP_CYCLE_EXCEPTION per robot.  Returns 0, MGQP_CYCLE_NO_DATA /
+ * MGQP_CYCLE_NO_JACOBIAN when the whole batch exits early like updateHook (nothing written),
+ * or -1 on an argument / GPU error (mgqp_last_error).  Bit-identical to mgqp_update_batched. */
+int mgqp_update_device(mgqp_ctl* c, const mgqp_device_batch* b, float* torques, float* tracking,
+                       int32_t* codes, void* stream);
+
 /* Z = I - V A V^T for Acumul (rows x cols), written as dim x dim. */
 void mgqp_nullspace_projector(const float* A, int32_t rows, int32_t cols, int32_t dim, float* Z);
 

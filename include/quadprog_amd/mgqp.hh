@@ -123,6 +123,11 @@ class MotionGenerationQuadraticProgram {
   // robot whose solve throws in the reference gets code CYCLE_EXCEPTION instead.
   void update_batched(const CycleInputs* in, CycleOutputs* out, long count, int threads = 0);
 
+  // Device-resident batch (include/mgqp_amd.h mgqp_device_batch; `batch` is that struct).
+  // Returns 0, CYCLE_NO_DATA / CYCLE_NO_JACOBIAN for a uniform early exit, or throws
+  // std::runtime_error / std::length_error.
+  int update_device(const void* batch, float* torques, float* tracking, int* codes, void* stream);
+
   // src/mgqp.cpp:655-749 and 751-869 (they operate on this->stack_of_tasks)
   bool solveNextStep(const MatF& A, const VecF& a, const MatF& B, const VecF& b, VecF* res);
   VecF solveNextHierarchy();

@@ -7,13 +7,11 @@
 #include <vector>
 
 #include "mgqp_amd.h"
+#include "mgqp_ctl.h"
 #include "quadprog_amd/mgqp.hh"
 
 using namespace mgqp_amd;
 
-struct mgqp_ctl {
-  MotionGenerationQuadraticProgram c;
-};
 
 namespace {
 
@@ -144,5 +142,7 @@ void mgqp_nullspace_projector(const float* A, int32_t rows, int32_t cols, int32_
 }
 
 const char* mgqp_last_error(void) { return g_err.c_str(); }
+
+void mgqp_capi_set_error(const char* msg) { g_err = msg; }
 
 }  // extern "C"

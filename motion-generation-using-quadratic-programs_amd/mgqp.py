@@ -82,6 +82,9 @@ def _bind(L):
         L.mgqp_update_batched.argtypes = [vp, ctypes.c_int64, vp, vp, vp, vp, i32]
         L.mgqp_update_batched.restype = ctypes.c_int
         L.mgqp_nullspace_projector.argtypes = [vp, i32, i32, i32, vp]
+        if hasattr(L, "mgqp_update_device"):
+            L.mgqp_update_device.argtypes = [vp, vp, vp, vp, vp, vp]
+            L.mgqp_update_device.restype = ctypes.c_int
         L.mgqp_last_error.restype = ctypes.c_char_p
     return L
 
@@ -89,7 +92,54 @@ def _bind(L):
 EXPORTED_SYMBOLS = ("mgqp_create", "mgqp_destroy", "mgqp_set_dof", "mgqp_set_gains",
                     "mgqp_set_torque_limits", "mgqp_set_acceleration_limits",
                     "mgqp_set_angular_limits", "mgqp_set_priority_level", "mgqp_update",
-                    "mgqp_update_batched", "mgqp_nullspace_projector", "mgqp_last_error")
+                    "mgqp_update_batched", "mgqp_update_device", "mgqp_nullspace_projector",
+                    "mgqp_last_error")
+
+MAX_DOF = 16
+_P = ctypes.c_void_p
+
+
+class DeviceBatchC(ctypes.Structure):
+    """include/mgqp_amd.h mgqp_device_batch."""
+    _fields_ = [("count", ctypes.c_int64), ("angles", _P), ("velocities", _P), ("h", _P),
+                ("inertia", _P), ("ts", (_P * 6) * MAX_DOF), ("js", (_P * 3) * MAX_DOF),
+                ("jacobian", _P * MAX_DOF), ("jacobian_dot", _P * MAX_DOF),
+                ("ts_len", ctypes.c_int32 * MAX_DOF), ("jac_rows", ctypes.c_int32 * MAX_DOF),
+                ("jac_cols", ctypes.c_int32 * MAX_DOF), ("status_len", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+class DeviceScenario:
+    """A Scenario uploaded to HBM (torch tensors, robot-major) plus the C struct pointing at it:
+    the input of Controller.update_device (the device-resident cycle)."""
+
+    def __init__(self, sc: Scenario, device="cuda"):
+        import torch
+
+        self.dof, self.count = sc.dof, sc.count
+        t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(device)
+        self.tensors = {"angles": t(sc.angles), "velocities": t(sc.velocities), "h": t(sc.h),
+                        "inertia": t(sc.inertia)}
+        self.ports = {k: t(v) for k, v in sc.ports.items()}
+        b = DeviceBatchC()
+        b.count = sc.count
+        ptr = lambda x: None if x is None else x.data_ptr()
+        for nm, x in self.tensors.items():
+            setattr(b, nm, ptr(x))
+        if sc.angles is not None:
+            b.status_len = sc.angles.shape[1]
+        ts_idx = {nm: i for i, nm in enumerate(TS_PORTS)}
+        js_idx = {nm: i for i, nm in enumerate(JS_PORTS)}
+        for (j, nm), x in self.ports.items():
+            if nm in ts_idx:
+                b.ts[j][ts_idx[nm]] = x.data_ptr()
+                b.ts_len[j] = x.shape[1]
+            elif nm in js_idx:
+                b.js[j][js_idx[nm]] = x.data_ptr()
+            else:
+                (b.jacobian if nm == "jacobian" else b.jacobian_dot)[j] = x.data_ptr()
+                b.jac_rows[j], b.jac_cols[j] = x.shape[1], x.shape[2]
+        self.c = b
 
 
 def _ptr(a: np.ndarray) -> int:
@@ -218,6 +268,28 @@ class Controller:
         if rc != 0:
             raise RuntimeError("mgqp_update_batched: " + self.last_error())
         return codes, tq, tr
+
+
+def _update_device(self, dsc: "DeviceScenario", out=None, stream=None):
+    """The device-resident cycle (mgqp_update_device).  Returns (rc, codes, torques, tracking)
+    as torch tensors on the scenario's device (enqueued on `stream`, not synchronised)."""
+    import torch
+
+    dev = next(iter(dsc.tensors.values())).device
+    if out is None:
+        out = (torch.empty((dsc.count, self.dof), dtype=torch.float32, device=dev),
+               torch.empty((dsc.count, 2 * self.dof), dtype=torch.float32, device=dev),
+               torch.empty(dsc.count, dtype=torch.int32, device=dev))
+    tq, tr, codes = out
+    rc = self._L.mgqp_update_device(self._h, ctypes.addressof(dsc.c), tq.data_ptr(),
+                                    tr.data_ptr() if tr is not None else None, codes.data_ptr(),
+                                    stream)
+    if rc < 0:
+        raise RuntimeError("mgqp_update_device: " + self.last_error())
+    return rc, codes, tq, tr
+
+
+Controller.update_device = _update_device
 
 
 def last_error() -> str:

@@ -167,3 +167,63 @@ def test_joint_space_levels(gpu, lib=LIB):
         assert codes[r] == code == 0
         if not o.ill_conditioned:
             _close(tr[r], otr)
+
+
+# --- device-resident cycle: must equal the host-orchestrated batch ----
+def _device_vs_batched(c_dev, c_host, sc):
+    import torch
+
+    codes_h, tq_h, tr_h = c_host.update_batched(sc)
+    dsc = mgqp.DeviceScenario(sc, "cuda")
+    rc, codes, tq, tr = c_dev.update_device(dsc)
+    torch.cuda.synchronize()
+    assert rc == 0
+    codes, tq, tr = codes.cpu().numpy(), tq.cpu().numpy(), tr.cpu().numpy()
+    np.testing.assert_array_equal(codes, codes_h)
+    ok = codes == 0
+    np.testing.assert_array_equal(tq[ok], tq_h[ok])
+    np.testing.assert_array_equal(tr[ok], tr_h[ok])
+    return codes
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_device_cycle_equals_batched(gpu, wide):
+    sc = mgqp.make_scenario(700, seed=41)
+    cd, ch = _ctl(), _ctl()
+    if wide:
+        _wide(cd)
+        _wide(ch)
+    codes = _device_vs_batched(cd, ch, sc)
+    assert (codes == 0).all()
+
+
+def test_device_cycle_edge_cases(gpu):
+    sc = mgqp.make_scenario(130, seed=43)
+    sc.angles[0, 0] = 0.8                  # log(0) = -inf limit
+    sc.angles[1, 2] = 2.7                  # NaN limit
+    sc.ports[(6, "jacobian")][5, 1] = 0    # dependent level-0 row -> exception for robot 5
+    codes = _device_vs_batched(_ctl(), _ctl(), sc)
+    assert codes[5] == mgqp.CYCLE_EXCEPTION and (np.delete(codes, 5) == 0).all()
+
+
+def test_device_cycle_joint_space_levels(gpu):
+    sc = mgqp.make_scenario(200, seed=47)
+    K = sc.count
+    sc.ports[(2, "desired_js_velocity")] = np.linspace(-0.3, 0.3, K).astype(np.float32)
+    sc.ports[(3, "desired_js_acceleration")] = np.linspace(-1, 1, K).astype(np.float32)
+    cs = [_ctl(), _ctl()]
+    for c in cs:
+        c.setPriorityLevel("in_desiredJointSpaceVelocity_3", 1)
+        c.setPriorityLevel("in_desiredJointSpaceAcceleration_4", 2)
+    _device_vs_batched(cs[0], cs[1], sc)
+
+
+def test_device_cycle_early_exits(gpu):
+    sc = mgqp.make_scenario(8, seed=2)
+    sc.h = None
+    rc, _, _, _ = _ctl().update_device(mgqp.DeviceScenario(sc, "cuda"))
+    assert rc == mgqp.CYCLE_NO_DATA
+    sc = mgqp.make_scenario(8, seed=2)
+    del sc.ports[(6, "jacobian")]
+    rc, _, _, _ = _ctl().update_device(mgqp.DeviceScenario(sc, "cuda"))
+    assert rc == mgqp.CYCLE_NO_JACOBIAN
