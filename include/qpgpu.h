@@ -120,6 +120,20 @@ int qpgpu_solve_batched(const qpgpu_problem_desc* d,
                         double* x, double* f, int32_t* status, int32_t* iters,
                         void* stream);
 
+/* Same as qpgpu_solve_batched, plus, per QP, the answer of the same problem with the
+ * inequality constraints dropped (m = 0): x_eq (n doubles, same layout as x), f_eq, status_eq.
+ * That is the state the full solve passes through after its equality phase, so it costs a
+ * few stores, and it is bit-identical to a separate qpgpu_solve_batched with m = 0.  This is
+ * the retry of reference src/mgqp.cpp:717-736 (solve_quadprog again with CI of 0 columns)
+ * folded into the first solve. */
+int qpgpu_solve_batched_eq(const qpgpu_problem_desc* d,
+                           double* G, const double* g0,
+                           const double* CE, const double* ce0,
+                           const double* CI, const double* ci0,
+                           double* x, double* f, int32_t* status, int32_t* iters,
+                           double* x_eq, double* f_eq, int32_t* status_eq,
+                           void* stream);
+
 /* Same, with HOST pointers: copies the inputs to the device, solves, copies the outputs back
  * and synchronises.  This is what the ArrayHH drop-in (libquadprog_amd.so) calls for each
  * solve_quadprog(); it always runs the HIP kernel (there is no CPU path in the product).

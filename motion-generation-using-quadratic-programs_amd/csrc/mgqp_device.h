@@ -63,6 +63,7 @@ struct Work {
   float* res;     // [dim][count]
   float* u;       // [dim][count]
   int32_t* state; // [count]: 0 active, 1 done (stopped at a level), 2 exception
+  double* V;      // [dim * dim][count]: thin right singular vectors of the projector
   const float* Bcumul;  // [nineq][dim] shared by all robots (limitsMatrix, :1083-1085)
 };
 

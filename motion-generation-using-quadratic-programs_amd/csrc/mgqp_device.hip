@@ -265,6 +265,174 @@ __global__ void finish_level_kernel(Plan P, Work W, const double* x1, const doub
   }
 }
 
+// ------------------------------------------------------------------ register-resident versions
+// For dim N <= 14 (DOF <= 7): Z lives in registers (N*N floats) and the Jacobi operand of the
+// common r < N case (X = Acumul^T, N x r, r <= N-1) too, fully unrolled over N and RMAX = N-1
+// with wave-uniform guards on the runtime row count.  Same operation order as the generic
+// kernels (and the host), so the results are bit-identical.
+template <int N>
+__global__ __launch_bounds__(64) void build_level_reg_kernel(Plan P, Work W, int row0, int p,
+                                                             double* CE, double* ce0, double* CI,
+                                                             double* ci0) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t K = W.count;
+  if (r >= K) return;
+  const int m = P.nineq;
+  float Z[N][N];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j) Z[i][j] = ld(W.Z, i * N + j, K, r);
+  float res[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) res[i] = ld(W.res, i, K, r);
+  double* CEr = CE + r * N * p;
+  for (int i = 0; i < p; ++i) {
+    const int64_t crow = (int64_t)(row0 + i) * N;
+    float c[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) c[k] = ld(W.cond, crow + k, K, r);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < N; ++k) sum += c[k] * Z[k][j];
+      CEr[j * p + i] = (double)sum;
+    }
+    float cl = 0.f;
+#pragma unroll
+    for (int k = 0; k < N; ++k) cl += c[k] * res[k];
+    ce0[r * p + i] = (double)(ld(W.goal, row0 + i, K, r) - cl);
+  }
+  double* CIr = CI + r * N * m;
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < m; ++i) {
+      const float* b = W.Bcumul + i * N;
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < N; ++k) sum += b[k] * Z[k][j];
+      CIr[j * m + i] = (double)sum;
+    }
+  for (int i = 0; i < m; ++i) ci0[r * m + i] = (double)ld(W.limits, i, K, r);
+}
+
+template <int N, int R>
+__global__ __launch_bounds__(64) void finish_level_reg_kernel(Plan P, Work W, const double* x1,
+                                                              const double* f1, const int32_t* st1,
+                                                              const double* x2, const double* f2,
+                                                              const int32_t* st2, int acc_rows) {
+  constexpr int RM = R;  // exact stacked row count (< N): X = Acumul^T is N x R
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t K = W.count;
+  if (r >= K) return;
+  if (W.state[r] != 0) return;
+  bool ok = true, exc = false;
+  const int s1 = st1[r];
+  const double* xs = x1;
+  if (s1 == QPGPU_QP_DEPENDENT || s1 == QPGPU_QP_MAX_ITER) {
+    exc = true;
+  } else if (bad_f(f1[r])) {
+    const int s2 = st2[r];
+    if (s2 == QPGPU_QP_DEPENDENT || s2 == QPGPU_QP_MAX_ITER) exc = true;
+    else if (!bad_f(f2[r])) xs = x2;
+    else ok = false;
+  }
+  if (exc) {
+    W.state[r] = 2;
+    return;
+  }
+  float u[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) u[i] = ok ? (float)xs[r * N + i] : 0.f;
+#pragma unroll
+  for (int i = 0; i < N; ++i) W.u[(int64_t)i * K + r] = u[i];
+  if (!ok) {
+    W.state[r] = 1;
+    return;
+  }
+  {
+    float zu[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < N; ++k) sum += ld(W.Z, i * N + k, K, r) * u[k];
+      zu[i] = sum;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) W.res[(int64_t)i * K + r] = ld(W.res, i, K, r) + zu[i];
+  }
+  if (acc_rows <= 0) return;
+  (void)acc_rows;  // == R (checked by the launcher)
+  constexpr int rr = R;
+  double X[N][RM];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < RM; ++j) X[i][j] = j < rr ? (double)ld(W.cond, (int64_t)j * N + i, K, r) : 0.0;
+  for (int sweep = 0; sweep < 80; ++sweep) {
+    bool rotated = false;
+#pragma unroll
+    for (int p = 0; p < RM - 1; ++p)
+#pragma unroll
+      for (int q = p + 1; q < RM; ++q) {
+        double al = 0, be = 0, ga = 0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          al += X[i][p] * X[i][p];
+          be += X[i][q] * X[i][q];
+          ga += X[i][p] * X[i][q];
+        }
+        if (ga == 0.0 || fabs(ga) <= 1e-15 * sqrt(al * be)) continue;
+        rotated = true;
+        const double zeta = (be - al) / (2.0 * ga);
+        const double tt = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        const double c = 1.0 / sqrt(1.0 + tt * tt), sn = c * tt;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          const double a0 = X[i][p], b0 = X[i][q];
+          X[i][p] = c * a0 - sn * b0;
+          X[i][q] = sn * a0 + c * b0;
+        }
+      }
+    if (!rotated) break;
+  }
+  // thin V (normalised columns; dropped singular values zeroed, which leaves the host's sums
+  // unchanged) to the V workspace; zform_kernel forms Z from it
+#pragma unroll
+  for (int j = 0; j < RM; ++j) {
+    double nrm = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) nrm += X[i][j] * X[i][j];
+    const double sg = sqrt(nrm);
+    const bool keep = !((double)(float)sg < 0.0000000000000001);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      W.V[((int64_t)i * RM + j) * K + r] = keep && sg > 0 ? X[i][j] / sg : 0.0;
+  }
+}
+
+// Z = I - V V^T from the V workspace (rows of V: N, columns: R), for robots still active.
+template <int N>
+__global__ __launch_bounds__(64) void zform_kernel(Work W, int R) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t K = W.count;
+  if (r >= K || W.state[r] != 0) return;
+  for (int i = 0; i < N; ++i) {
+    double vi[N];
+#pragma unroll
+    for (int l = 0; l < N; ++l) vi[l] = l < R ? W.V[((int64_t)i * R + l) * K + r] : 0.0;
+    for (int j = 0; j < N; ++j) {
+      double sum = 0;
+#pragma unroll
+      for (int l = 0; l < N; ++l)
+        if (l < R) sum += vi[l] * W.V[((int64_t)j * R + l) * K + r];
+      W.Z[((int64_t)i * N + j) * K + r] = (i == j ? 1.f : 0.f) - (float)sum;
+    }
+  }
+}
+
 __global__ void outputs_kernel(Plan P, Work W, float* torques, float* tracking, int32_t* codes) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t K = W.count;
@@ -296,8 +464,34 @@ int launch_build_tasks(const Plan& P, const Work& W, hipStream_t s) {
   return check(hipGetLastError());
 }
 
+template <int N>
+bool try_build_level_reg(const Plan& P, const Work& W, int level, double* CE, double* ce0,
+                         double* CI, double* ci0, hipStream_t s) {
+  if (P.dim != N) return false;
+  hipLaunchKernelGGL(build_level_reg_kernel<N>, grid_for(W.count, 64), dim3(64), 0, s, P, W,
+                     P.level_row0[level], P.level_rows[level], CE, ce0, CI, ci0);
+  return true;
+}
+
+template <int N, int R>
+bool try_finish_level_reg(const Plan& P, const Work& W, const double* x1, const double* f1,
+                          const int32_t* st1, const double* x2, const double* f2,
+                          const int32_t* st2, int acc_rows, hipStream_t s) {
+  if (P.dim != N || acc_rows != R) return false;
+  hipLaunchKernelGGL((finish_level_reg_kernel<N, R>), grid_for(W.count, 64), dim3(64), 0, s, P,
+                     W, x1, f1, st1, x2, f2, st2, acc_rows);
+  hipLaunchKernelGGL(zform_kernel<N>, grid_for(W.count, 64), dim3(64), 0, s, W, R);
+  return true;
+}
+
 int launch_build_level(const Plan& P, const Work& W, int level, double* CE, double* ce0,
                        double* CI, double* ci0, hipStream_t s) {
+  if (try_build_level_reg<14>(P, W, level, CE, ce0, CI, ci0, s) ||
+      try_build_level_reg<12>(P, W, level, CE, ce0, CI, ci0, s) ||
+      try_build_level_reg<10>(P, W, level, CE, ce0, CI, ci0, s) ||
+      try_build_level_reg<8>(P, W, level, CE, ce0, CI, ci0, s) ||
+      try_build_level_reg<6>(P, W, level, CE, ce0, CI, ci0, s))
+    return check(hipGetLastError());
   hipLaunchKernelGGL(build_level_kernel, grid_for(W.count, 256), dim3(256), 0, s, P, W,
                      P.level_row0[level], P.level_rows[level], CE, ce0, CI, ci0);
   return check(hipGetLastError());
@@ -307,6 +501,14 @@ int launch_finish_level(const Plan& P, const Work& W, int level, const double* x
                         const double* f1, const int32_t* st1, const double* x2, const double* f2,
                         const int32_t* st2, int acc_rows, hipStream_t s) {
   (void)level;
+  // DOF 7 (the reference robot): the stacked row counts of its usual stacks
+  if (try_finish_level_reg<14, 10>(P, W, x1, f1, st1, x2, f2, st2, acc_rows, s) ||
+      try_finish_level_reg<14, 11>(P, W, x1, f1, st1, x2, f2, st2, acc_rows, s) ||
+      try_finish_level_reg<14, 12>(P, W, x1, f1, st1, x2, f2, st2, acc_rows, s) ||
+      try_finish_level_reg<14, 7>(P, W, x1, f1, st1, x2, f2, st2, acc_rows, s) ||
+      try_finish_level_reg<14, 8>(P, W, x1, f1, st1, x2, f2, st2, acc_rows, s) ||
+      try_finish_level_reg<14, 9>(P, W, x1, f1, st1, x2, f2, st2, acc_rows, s))
+    return check(hipGetLastError());
   const int c = P.dim;
   const size_t per = acc_rows > 0 ? ((size_t)acc_rows * c + (acc_rows >= c ? (size_t)c * c : 0)) * 8
                                   : 0;
@@ -364,6 +566,7 @@ int run_cycle(const Plan& P, int64_t K, const float* Bcumul_host, float* torques
   const size_t oCond = take(fK * P.total_rows * n * 4), oGoal = take(fK * P.total_rows * 4),
                oLim = take(fK * m * 4), oZ = take(fK * n * n * 4), oRes = take(fK * n * 4),
                oU = take(fK * n * 4), oState = take(fK * 4), oB = take((size_t)m * n * 4),
+               oV = take(fK * n * n * 8),
                oG = take(fK * n * n * 8), og0 = take(fK * n * 8), oCE = take(fK * n * pmax * 8),
                oce0 = take(fK * pmax * 8), oCI = take(fK * n * m * 8), oci0 = take(fK * m * 8),
                ox1 = take(fK * n * 8), of1 = take(fK * 8), os1 = take(fK * 4),
@@ -391,6 +594,7 @@ int run_cycle(const Plan& P, int64_t K, const float* Bcumul_host, float* torques
   W.u = reinterpret_cast<float*>(b + oU);
   W.state = reinterpret_cast<int32_t*>(b + oState);
   W.Bcumul = reinterpret_cast<float*>(b + oB);
+  W.V = reinterpret_cast<double*>(b + oV);
   double *G = reinterpret_cast<double*>(b + oG), *g0 = reinterpret_cast<double*>(b + og0),
          *CE = reinterpret_cast<double*>(b + oCE), *ce0 = reinterpret_cast<double*>(b + oce0),
          *CI = reinterpret_cast<double*>(b + oCI), *ci0 = reinterpret_cast<double*>(b + oci0),
@@ -419,16 +623,12 @@ int run_cycle(const Plan& P, int64_t K, const float* Bcumul_host, float* torques
     d.p = p;
     d.m = m;
     d.batch = K;
-    int rc = qpgpu_solve_batched(&d, G, g0, CE, ce0, CI, ci0, x1, f1, s1, nullptr, s);
+    // one launch gives both the solve with CI and the retry without it (:717-736): the latter
+    // is the state after the equality phase (qpgpu_solve_batched_eq)
+    const int rc = qpgpu_solve_batched_eq(&d, G, g0, CE, ce0, CI, ci0, x1, f1, s1, nullptr, x2,
+                                          f2, s2, s);
     if (rc != QPGPU_SUCCESS) {
-      g_cws.err = std::string("qpgpu_solve_batched: ") + qpgpu_last_error();
-      *err = g_cws.err.c_str();
-      return -3;
-    }
-    d.m = 0;  // the retry without inequalities (:723-725)
-    rc = qpgpu_solve_batched(&d, G, g0, CE, ce0, nullptr, nullptr, x2, f2, s2, nullptr, s);
-    if (rc != QPGPU_SUCCESS) {
-      g_cws.err = std::string("qpgpu_solve_batched (retry): ") + qpgpu_last_error();
+      g_cws.err = std::string("qpgpu_solve_batched_eq: ") + qpgpu_last_error();
       *err = g_cws.err.c_str();
       return -3;
     }

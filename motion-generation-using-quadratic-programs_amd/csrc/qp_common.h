@@ -69,6 +69,11 @@ struct QpArgs {
   double* f;
   int32_t* status;
   int32_t* iters;
+  // optional (NULL unless qpgpu_solve_batched_eq): the state after the equality phase, i.e. the
+  // result of the same QP with CI dropped (m = 0) — x_eq / f_eq / st_eq per QP
+  double* x_eq;
+  double* f_eq;
+  int32_t* st_eq;
   // diagnostic only (NULL in every product call): per-wave s_memtime stamps at phase
   // boundaries, kStampSlots per wave, written by lane 0.  Never feeds an output.
   uint64_t* stamps;

@@ -520,6 +520,19 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
       }
     }
   }
+  // the m = 0 answer (qpgpu_solve_batched_eq): an empty l1 scan returns right here.  Only the
+  // generic instantiations carry it; the launcher routes snapshot calls there so the EXACT
+  // fast paths keep their register budget.
+  if (!EXACT && a.x_eq && live) {
+    if (chol_ok) {
+      double* xb = view(a.x_eq, n);
+#pragma unroll
+      for (int i = 0; i < NM; i++)
+        if (i < n) xb[i * T] = xv[i];
+    }
+    a.f_eq[b] = fval;
+    a.st_eq[b] = status;
+  }
   qp_stamp(a, 2);
 
   // ---------------------------------------------------------------- active-set loop
@@ -816,7 +829,7 @@ template <int NM, int MM, int T, int QPW>
 static void launch_lane_t(const QpArgs& a, hipStream_t stream) {
   const int64_t blocks = (a.batch + QPW - 1) / QPW;
   const dim3 g((unsigned)blocks), blk(64);
-  if (a.n == NM && a.m == MM) {
+  if (a.n == NM && a.m == MM && !a.x_eq) {
     if (QPW == 64 && a.p == 6)
       hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, true, QPW, 6>), g, blk, 0, stream, a);
     else if (QPW == 64 && a.p == 0)

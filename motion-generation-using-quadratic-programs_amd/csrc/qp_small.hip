@@ -178,6 +178,10 @@ __global__ void __launch_bounds__(64) qp_small_kernel(const QpArgs a) {
     status = QPGPU_QP_NOT_POSITIVE_DEFINITE;
     fval = bad_sum;
     write_x = false;
+    if (a.x_eq && ls == 0) {
+      a.f_eq[b] = fval;
+      a.st_eq[b] = status;
+    }
   } else {
     // ---------------------------------------------------------------- J = L^{-T}
     double Jr[RPL][NM];
@@ -466,6 +470,15 @@ __global__ void __launch_bounds__(64) qp_small_kernel(const QpArgs a) {
       if (!add_constraint()) {
         status = QPGPU_QP_DEPENDENT;
         done = true;
+      }
+    }
+    if (a.x_eq) {  // the m = 0 answer: an empty l1 scan returns right here
+#pragma unroll
+      for (int i = 0; i < NM; i++)
+        if (i < n && (i % S) == ls) a.x_eq[qbase_rt(b, n, T) + (int64_t)i * T] = xv[i];
+      if (ls == 0) {
+        a.f_eq[b] = fval;
+        a.st_eq[b] = status;
       }
     }
 

@@ -454,6 +454,17 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
     ctl->phase = PH_DONE;
   }
   grp_sync<S>();
+  if (a.x_eq && live) {  // the m = 0 answer: an empty l1 scan returns right here
+    const int st = ctl->status;
+    if (st != QPGPU_QP_NOT_POSITIVE_DEFINITE) {
+      double* xb = a.x_eq + qbase_rt(bb, n, T);
+      for (int i = ls; i < n; i += S) EL(xb, i) = xv[i];
+    }
+    if (lead) {
+      a.f_eq[b] = ctl->f;
+      a.st_eq[b] = st;
+    }
+  }
 
   // ------------------------------------------------------------------ active-set loop
   // Per-subgroup state machine; a wave loops until all of its QPs are done.

@@ -135,10 +135,35 @@ const char* qpgpu_kernel_name(int32_t n, int32_t p, int32_t m) {
   return s ? s : "";
 }
 
+static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const double* g0,
+                              const double* CE, const double* ce0, const double* CI,
+                              const double* ci0, double* x, double* f, int32_t* status,
+                              int32_t* iters, double* x_eq, double* f_eq, int32_t* st_eq,
+                              void* stream);
+
 int qpgpu_solve_batched(const qpgpu_problem_desc* d, double* G, const double* g0,
                         const double* CE, const double* ce0, const double* CI,
                         const double* ci0, double* x, double* f, int32_t* status,
                         int32_t* iters, void* stream) {
+  return solve_batched_impl(d, G, g0, CE, ce0, CI, ci0, x, f, status, iters, nullptr, nullptr,
+                            nullptr, stream);
+}
+
+int qpgpu_solve_batched_eq(const qpgpu_problem_desc* d, double* G, const double* g0,
+                           const double* CE, const double* ce0, const double* CI,
+                           const double* ci0, double* x, double* f, int32_t* status,
+                           int32_t* iters, double* x_eq, double* f_eq, int32_t* status_eq,
+                           void* stream) {
+  if (!x_eq || !f_eq || !status_eq) return QPGPU_ERR_INVALID_ARGUMENT;
+  return solve_batched_impl(d, G, g0, CE, ce0, CI, ci0, x, f, status, iters, x_eq, f_eq,
+                            status_eq, stream);
+}
+
+static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const double* g0,
+                              const double* CE, const double* ce0, const double* CI,
+                              const double* ci0, double* x, double* f, int32_t* status,
+                              int32_t* iters, double* x_eq, double* f_eq, int32_t* st_eq,
+                              void* stream) {
   int rc = validate(d);
   if (rc) return rc;
   if (d->batch == 0) return QPGPU_SUCCESS;
@@ -163,6 +188,9 @@ int qpgpu_solve_batched(const qpgpu_problem_desc* d, double* G, const double* g0
   a.f = f;
   a.status = status;
   a.iters = iters;
+  a.x_eq = x_eq;
+  a.f_eq = f_eq;
+  a.st_eq = st_eq;
   a.stamps = g_stamps;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int handled = 0;

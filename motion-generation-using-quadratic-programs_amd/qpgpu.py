@@ -55,6 +55,7 @@ LAYOUTS = {None: 0, "qp_major": LAYOUT_QP_MAJOR, "tiled64": LAYOUT_TILED64}
 
 EXPORTED_SYMBOLS = (
     "qpgpu_solve_batched",
+    "qpgpu_solve_batched_eq",
     "qpgpu_solve_batched_host",
     "qpgpu_max_n",
     "qpgpu_max_m",
@@ -91,6 +92,8 @@ def _load():
     vp = ctypes.c_void_p
     lib.qpgpu_solve_batched.argtypes = [ctypes.POINTER(ProblemDesc)] + [vp] * 11
     lib.qpgpu_solve_batched.restype = ctypes.c_int
+    lib.qpgpu_solve_batched_eq.argtypes = [ctypes.POINTER(ProblemDesc)] + [vp] * 14
+    lib.qpgpu_solve_batched_eq.restype = ctypes.c_int
     lib.qpgpu_solve_batched_host.argtypes = [ctypes.POINTER(ProblemDesc)] + [vp] * 10
     lib.qpgpu_solve_batched_host.restype = ctypes.c_int
     lib.qpgpu_kernel_name.argtypes = [ctypes.c_int32] * 3
@@ -240,8 +243,11 @@ class DeviceBatch:
         self.status = torch.zeros(self.batch, dtype=torch.int32, device=device)
         self.iters = torch.zeros(self.batch, dtype=torch.int32, device=device) if with_iters else None
 
-    def solve(self, stream=None, max_iter: int = 0, write_factor: bool = False, family=None):
-        """Enqueue one batched solve on `stream` (a torch.cuda.Stream, default current)."""
+    def solve(self, stream=None, max_iter: int = 0, write_factor: bool = False, family=None,
+              eq_out=None):
+        """Enqueue one batched solve on `stream` (a torch.cuda.Stream, default current).
+        eq_out=(x_eq, f_eq, status_eq) tensors also receive the m = 0 answer
+        (qpgpu_solve_batched_eq)."""
         import torch
 
         if stream is None:
@@ -249,10 +255,13 @@ class DeviceBatch:
         d = ProblemDesc(self.n, self.p, self.m, max_iter, self.batch,
                         (FLAG_WRITE_FACTOR if write_factor else 0) | FAMILY_FLAGS[family], self.layout)
         vp = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
-        rc = LIB.qpgpu_solve_batched(ctypes.byref(d), vp(self.G), vp(self.g0), vp(self.CE),
-                                     vp(self.ce0), vp(self.CI), vp(self.ci0), vp(self.x), vp(self.f),
-                                     vp(self.status), vp(self.iters),
-                                     ctypes.c_void_p(stream.cuda_stream))
+        args = [ctypes.byref(d), vp(self.G), vp(self.g0), vp(self.CE), vp(self.ce0), vp(self.CI),
+                vp(self.ci0), vp(self.x), vp(self.f), vp(self.status), vp(self.iters)]
+        if eq_out is None:
+            rc = LIB.qpgpu_solve_batched(*args, ctypes.c_void_p(stream.cuda_stream))
+        else:
+            rc = LIB.qpgpu_solve_batched_eq(*args, *[vp(t) for t in eq_out],
+                                            ctypes.c_void_p(stream.cuda_stream))
         _check(rc, "qpgpu_solve_batched")
 
     def results(self):

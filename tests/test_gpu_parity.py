@@ -168,3 +168,41 @@ def test_device_relayout_roundtrip(gpu):
         torch.cuda.synchronize()
         assert np.array_equal(t.cpu().numpy(), qpgpu.to_tiled64(a))
         assert np.array_equal(back.cpu().numpy(), a)
+
+
+@pytest.mark.parametrize("family", FAMILIES)
+@pytest.mark.parametrize("layout", ["qp_major", "tiled64"])
+@pytest.mark.parametrize("kind,n,p,m", [("general", 7, 6, 14), ("general", 14, 10, 28),
+                                        ("general", 14, 1, 28), ("general", 30, 6, 60),
+                                        ("box", 7, 0, 14), ("general", 5, 7, 6)])
+def test_eq_snapshot_equals_m0_solve(gpu, family, layout, kind, n, p, m):
+    """qpgpu_solve_batched_eq: the m = 0 answer written after the equality phase must equal a
+    separate solve with the inequalities dropped (the reference's retry, src/mgqp.cpp:723),
+    bit for bit — checked against the oracle."""
+    import torch
+
+    if not covers(family, n, m):
+        pytest.skip("family does not cover the shape")
+    pr = qpgpu.make_problems(kind, n, p, m, 0, 777, seed=5)
+    lay = qpgpu.LAYOUTS[layout]
+    db = qpgpu.DeviceBatch(pr, "cuda:0", with_iters=True, layout=layout)
+    xe = torch.full_like(db.x, float("nan"))
+    fe = torch.empty_like(db.f)
+    se = torch.empty_like(db.status)
+    db.solve(family=family, eq_out=(xe, fe, se))
+    torch.cuda.synchronize()
+    x, f, st, it = db.results()
+    # the full solve is unchanged by the extra outputs
+    xo, fo, so, io = oracle.solve_batch(pr, max_steps=1000 + 100 * (n + p + m))
+    assert np.array_equal(so, st) and np.array_equal(fo.view(np.uint64), f.view(np.uint64))
+    # the snapshot against the oracle's m = 0 solve
+    pr0 = qpgpu.Problems(n, p, 0, pr.G.copy(), pr.g0, pr.CE, pr.ce0, np.zeros((pr.batch, n, 0)),
+                         np.zeros((pr.batch, 0)))
+    x0, f0, s0, _ = oracle.solve_batch(pr0)
+    xe = xe.cpu().numpy()
+    if lay == qpgpu.LAYOUT_TILED64:
+        xe = qpgpu.from_tiled64(xe.reshape(-1), pr.batch, (n,))
+    assert np.array_equal(se.cpu().numpy(), s0)
+    assert np.array_equal(fe.cpu().numpy().view(np.uint64), f0.view(np.uint64))
+    ok = s0 != qpgpu.QP_NOT_POSITIVE_DEFINITE
+    assert np.array_equal(xe[ok].view(np.uint64), x0[ok].view(np.uint64))
