@@ -3,9 +3,17 @@
 
 One "step" = one batched solve (one launch of the gfx950 kernel through the C-ABI
 qpgpu_solve_batched) over the rank's resident batch of synthetic QPs, plus — when N > 1 — the
-RCCL gather of that step's results (x, f, status) to rank 0, run on a separate stream and
-double-buffered so it overlaps the next step's solve.  Inputs are generated on the host from
-the counter-based generator (qpgpu.make_problems) and copied to HBM before timing.
+RCCL gather of that step's results (x, f, status) to rank 0 on a separate stream.  Inputs are
+generated on the host from the counter-based generator (qpgpu.make_problems) and copied to HBM
+before timing.
+
+Steps are independent batches (one control period's QPs each), so they are pipelined: step k is
+enqueued on HIP stream k mod S (--streams, default 3: GPU_MAX_HW_QUEUES is 4 and a fourth
+stream measured sharing a hardware queue) with its own output buffers.  With 65 536
+QPs a launch is exactly one wave per SIMD, so a single launch ends with most SIMDs idle behind
+its slowest waves; the next step's waves fill them.  `value` is the pipelined whole-job
+throughput; `roofline` uses the kernel's own duration from a separate serialized pass (HIP events
+around each launch, one stream), which is what `rocprofv3 ... bench.py --streams 1` reports.
 
 Default workload = BASELINE.json's metric config: 65 536 x (n=7, p=6, m=14) per GPU (weak
 scaling: per-GPU work is fixed as N grows; C4's 1M QPs on 8 GPUs is --batch 131072 --gpus 8).
@@ -54,6 +62,10 @@ def parse():
     ap.add_argument("--layout", default="qp_major", choices=["qp_major", "tiled64"],
                     help="batch layout of the resident inputs (include/qpgpu.h)")
     ap.add_argument("--no-gather", action="store_true", help="skip the rank-0 result gather (N>1)")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="HIP streams the steps are pipelined over (1 = serialized launches)")
+    ap.add_argument("--kernel-reps", type=int, default=20,
+                    help="serialized launches timed for the roofline's kernel duration")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -115,47 +127,52 @@ def main():
                  "wave": f"qp_wave[n={n},m={m}]"}[args.family]
     if not kname:
         sys.exit(f"no gfx950 kernel covers (n, p, m) = {(n, p, m)}")
-    bufs = [qpgpu.DeviceBatch(pr, dev, with_iters=False, layout=args.layout)]
+    base = qpgpu.DeviceBatch(pr, dev, with_iters=False, layout=args.layout)
+    S = max(1, args.streams)
     gather = world > 1 and not args.no_gather
-    if gather:  # second output set for double buffering against the in-flight gather
-        b2 = qpgpu.DeviceBatch.__new__(qpgpu.DeviceBatch)
-        b2.__dict__.update(bufs[0].__dict__)
-        b2.x = torch.empty_like(bufs[0].x)
-        b2.f = torch.empty_like(bufs[0].f)
-        b2.status = torch.empty_like(bufs[0].status)
-        bufs.append(b2)
-        rows = bufs[0].x.shape[0]
+
+    def out_set():  # same resident inputs, private outputs
+        b = qpgpu.DeviceBatch.__new__(qpgpu.DeviceBatch)
+        b.__dict__.update(base.__dict__)
+        b.x = torch.empty_like(base.x)
+        b.f = torch.empty_like(base.f)
+        b.status = torch.empty_like(base.status)
+        return b
+
+    bufs = [base] + [out_set() for _ in range(S - 1)]
+    streams = [torch.cuda.Stream(dev) for _ in range(S)]  # non-default streams (no implicit sync)
+    if gather:
+        rows = base.x.shape[0]
         pdev = dev if backend == "nccl" else torch.device("cpu")
-        packed = [torch.empty((rows, n + 2), dtype=torch.float64, device=pdev) for _ in range(2)]
+        packed = [torch.empty((rows, n + 2), dtype=torch.float64, device=pdev) for _ in range(S)]
         recv = [torch.empty((rows, n + 2), dtype=torch.float64, device=pdev) for _ in range(world)] if rank == 0 else None
         comm = torch.cuda.Stream(dev)
-        works = [None, None]
-    compute = torch.cuda.current_stream(dev)
+        works = [None] * S
 
-    def step(k, ev=None):
-        db = bufs[k % len(bufs)]
-        if gather and works[k % 2] is not None:
-            works[k % 2].wait()  # compute stream waits until that buffer's gather finished
-            works[k % 2] = None
-        if ev:
-            ev[0].record(compute)
-        db.solve(stream=compute, family=args.family)
-        if ev:
-            ev[1].record(compute)
+    launch = [bufs[j].launcher(streams[j], family=args.family) for j in range(S)]
+
+    def step(k):
+        j = k % S
+        db, cs = bufs[j], streams[j]
+        if gather and works[j] is not None:
+            works[j].wait()  # this stream's outputs are free once their gather finished
+            works[j] = None
+        launch[j]()
         if gather:
-            # pack (x, f, status) and gather to rank 0 on the comm stream, overlapping the next
-            # step's solve (double-buffered outputs)
-            pk = packed[k % 2]
-            if backend == "nccl":
-                pk.copy_(qpdist.pack_results(db.x, db.f, db.status))
-                done = torch.cuda.Event()
-                done.record(compute)
-                with torch.cuda.stream(comm):
-                    comm.wait_event(done)
-                    works[k % 2] = dist.gather(pk, recv if rank == 0 else None, dst=0, async_op=True)
-            else:
-                pk.copy_(qpdist.pack_results(db.x, db.f, db.status).cpu())
-                works[k % 2] = dist.gather(pk, recv if rank == 0 else None, dst=0, async_op=True)
+            # pack (x, f, status) and gather to rank 0 on the comm stream, overlapping the
+            # following steps' solves
+            pk = packed[j]
+            with torch.cuda.stream(cs):
+                if backend == "nccl":
+                    pk.copy_(qpdist.pack_results(db.x, db.f, db.status))
+                    done = torch.cuda.Event()
+                    done.record(cs)
+                    with torch.cuda.stream(comm):
+                        comm.wait_event(done)
+                        works[j] = dist.gather(pk, recv if rank == 0 else None, dst=0, async_op=True)
+                else:
+                    pk.copy_(qpdist.pack_results(db.x, db.f, db.status).cpu())
+                    works[j] = dist.gather(pk, recv if rank == 0 else None, dst=0, async_op=True)
 
     for k in range(args.warmup):
         step(k)
@@ -163,11 +180,9 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(args.warmup + k, (starts[k], ends[k]))
+        step(args.warmup + k)
     if gather:
         for w in works:
             if w is not None:
@@ -177,8 +192,17 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    # kernel-only durations: HIP events bracketing each launch on the stream it runs on
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    # kernel-only duration for the roofline: serialized launches on one stream, HIP events
+    # bracketing each launch on the stream it runs on (untimed for `value`)
+    cs = streams[0]
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.kernel_reps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.kernel_reps)]
+    for r in range(args.kernel_reps):
+        starts[r].record(cs)
+        launch[0]()
+        ends[r].record(cs)
+    torch.cuda.synchronize(dev)
+    kern_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in zip(starts, ends)]))
     if dist:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -218,10 +242,12 @@ def main():
         "data": "synthetic",
         "config": {"workload": desc, "kind": kind, "n": n, "p": p, "m": m, "batch_per_gpu": B,
                    "global_batch": B * world, "kernel": kname, "layout": args.layout,
+                   "streams": S,
                    "parallelism": f"batch-sharded x{world}" + (", RCCL gather to rank 0 (overlapped)" if gather else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel_ms": kern_ms, "algorithmic_bytes_per_qp": bpq,
+                     "kernel_ms": kern_ms, "kernel_ms_source": "serialized launches, HIP events",
+                     "algorithmic_bytes_per_qp": bpq,
                      "traffic_source": traffic_src},
         "status_ok_frac": float((st == qpgpu.QP_OK).mean()),
     }
