@@ -31,12 +31,14 @@ for s in $STEPS; do
     benchfam)
       for f in ${FAMILIES:-lane subgroup}; do for l in qp_major tiled64; do run bench_${f}_$l 600 python bench.py --family $f --layout $l --no-cpu; done; done ;;
     benchall)
-      for c in C1 C2 mgqp C3; do run bench_$c 600 python bench.py --config $c --no-cpu; done
+      for c in C1 C2 mgqp C3; do run bench_$c 600 python bench.py --config $c --no-cpu --steps 20; done
       run bench_C5 600 python bench.py --config C5 --no-cpu --steps 3 --warmup 1 ;;
-    prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c1 -- python3 bench.py --steps 20 --warmup 5 --no-cpu ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c1 -- python3 bench.py --steps 20 --warmup 5 --no-cpu --streams 1 ;;
+    profmgqp) run profmgqp 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profmgqp" -o mgqp -- python3 tools/bench_mgqp.py --steps 3 --no-host --no-cpu ;;
+    benchmgqp) run benchmgqp 600 python tools/bench_mgqp.py ;;
     pmc)
-      run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu
-      run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu
+      run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --streams 1
+      run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --streams 1
       python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" C1 65536 "$(python3 -c 'import sys; sys.path.insert(0,"motion-generation-using-quadratic-programs_amd"); import qpgpu; print(qpgpu.kernel_name(7,6,14))')" "$OUT/pmc_traffic.json" ;;
     benchj)
       for j in 0 1; do for l in qp_major tiled64; do QPGPU_LANE_JREG=$j run bench_jreg${j}_$l 600 python bench.py --family lane --layout $l --no-cpu; done; done ;;
