@@ -155,7 +155,10 @@ def main():
         j = k % S
         db, cs = bufs[j], streams[j]
         if gather and works[j] is not None:
-            works[j].wait()  # this stream's outputs are free once their gather finished
+            # this stream's packed buffer is free once its gather finished: make stream cs
+            # wait for it (Work.wait() syncs the *current* stream with an nccl work)
+            with torch.cuda.stream(cs):
+                works[j].wait()
             works[j] = None
         launch[j]()
         if gather:
