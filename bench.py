@@ -2,8 +2,10 @@
 """Benchmark: batched Goldfarb–Idnani QP solves on MI355X (BASELINE.json metric).
 
 One "step" = one batched solve (one launch of the gfx950 kernel through the C-ABI
-qpgpu_solve_batched) over the rank's resident batch of synthetic QPs, plus — when N > 1 — the
-RCCL gather of that step's results (x, f, status) to rank 0 on a separate stream.  Inputs are
+qpgpu_solve_batched) over the rank's resident batch of synthetic QPs.  With N > 1 every rank
+solves its own shard (weak scaling, no data-path collective: the QPs are independent);
+--gather adds an RCCL gather of each step's results (x, f, status) to rank 0 on a separate
+stream, overlapped with the following solves, for deployments that collect results centrally.  Inputs are
 generated on the host from the counter-based generator (qpgpu.make_problems) and copied to HBM
 before timing.
 
@@ -61,7 +63,9 @@ def parse():
                     help="force a kernel family (default: the dispatcher's choice)")
     ap.add_argument("--layout", default="qp_major", choices=["qp_major", "tiled64"],
                     help="batch layout of the resident inputs (include/qpgpu.h)")
-    ap.add_argument("--no-gather", action="store_true", help="skip the rank-0 result gather (N>1)")
+    ap.add_argument("--gather", action="store_true",
+                    help="also gather every step's (x, f, status) to rank 0 over RCCL (N>1); off "
+                         "by default: the QPs are independent, so the path has no exchange step")
     ap.add_argument("--streams", type=int, default=3,
                     help="HIP streams the steps are pipelined over (1 = serialized launches)")
     ap.add_argument("--kernel-reps", type=int, default=20,
@@ -129,7 +133,7 @@ def main():
         sys.exit(f"no gfx950 kernel covers (n, p, m) = {(n, p, m)}")
     base = qpgpu.DeviceBatch(pr, dev, with_iters=False, layout=args.layout)
     S = max(1, args.streams)
-    gather = world > 1 and not args.no_gather
+    gather = world > 1 and args.gather
 
     def out_set():  # same resident inputs, private outputs
         b = qpgpu.DeviceBatch.__new__(qpgpu.DeviceBatch)
@@ -246,7 +250,7 @@ def main():
         "config": {"workload": desc, "kind": kind, "n": n, "p": p, "m": m, "batch_per_gpu": B,
                    "global_batch": B * world, "kernel": kname, "layout": args.layout,
                    "streams": S,
-                   "parallelism": f"batch-sharded x{world}" + (", RCCL gather to rank 0 (overlapped)" if gather else "")},
+                   "parallelism": f"batch-sharded x{world}" + (", RCCL gather to rank 0 (overlapped)" if gather else ", no collective")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms": kern_ms, "kernel_ms_source": "serialized launches, HIP events",
