@@ -109,8 +109,11 @@ typedef struct qpgpu_problem_desc {
 
 /* Solve `d->batch` independent QPs.  Every pointer is DEVICE memory (hipMalloc'd or a torch
  * tensor's data_ptr on the current device); `stream` is a hipStream_t (NULL = default stream).
- * The call only enqueues work: it does not synchronise and allocates nothing, so it can be
- * captured into a hipGraph.  G is read-only unless QPGPU_FLAG_WRITE_FACTOR is set.
+ * The call only enqueues work and does not synchronise, so it can be captured into a hipGraph.
+ * Shapes with n > 64 (J and R in global memory) use a device workspace cached per
+ * (device, stream): the first call on a stream allocates it (do that before capturing), and
+ * launches on different streams never share one.  G is read-only unless
+ * QPGPU_FLAG_WRITE_FACTOR is set.
  * `iters` (l1 passes per QP, the reference's `iter`) may be NULL.
  * Replaces: the per-QP call at reference src/mgqp.cpp:708, batched. */
 int qpgpu_solve_batched(const qpgpu_problem_desc* d,

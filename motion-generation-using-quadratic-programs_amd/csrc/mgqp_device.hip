@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <map>
 #include <mutex>
 #include <string>
 
@@ -533,19 +534,20 @@ namespace mgqp_dev {
 
 namespace {
 
+// Workspace per (device, stream): cycles enqueued on different streams never share one.
 struct CycleWs {
-  std::mutex mu;
-  int device = -1;
   size_t bytes = 0;
   void* buf = nullptr;
   int64_t qp_count = -1;  // G / g0 initialised for this (count, dim)
   int qp_dim = -1;
-  std::string err;
-} g_cws;
+};
+std::mutex g_cws_mu;
+std::map<std::pair<int, hipStream_t>, CycleWs> g_cws_map;
+thread_local std::string g_cws_err;
 
 int fail(const char* what, hipError_t e, const char** err) {
-  g_cws.err = std::string(what) + ": " + hipGetErrorString(e);
-  *err = g_cws.err.c_str();
+  g_cws_err = std::string(what) + ": " + hipGetErrorString(e);
+  *err = g_cws_err.c_str();
   return -1;
 }
 
@@ -553,7 +555,6 @@ int fail(const char* what, hipError_t e, const char** err) {
 
 int run_cycle(const Plan& P, int64_t K, const float* Bcumul_host, float* torques, float* tracking,
               int32_t* codes, hipStream_t s, const char** err) {
-  std::lock_guard<std::mutex> lock(g_cws.mu);
   if (K <= 0) return 0;
   const int n = P.dim, m = P.nineq;
   int pmax = 0;
@@ -574,14 +575,18 @@ int run_cycle(const Plan& P, int64_t K, const float* Bcumul_host, float* torques
   hipError_t e;
   int dev = 0;
   if ((e = hipGetDevice(&dev)) != hipSuccess) return fail("hipGetDevice", e, err);
-  if (g_cws.device != dev || g_cws.bytes < off) {
-    if (g_cws.buf) (void)hipFree(g_cws.buf);
+  std::lock_guard<std::mutex> lock(g_cws_mu);
+  CycleWs& g_cws = g_cws_map[{dev, s}];
+  if (g_cws.bytes < off) {
+    if (g_cws.buf) {
+      if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail("hipStreamSynchronize", e, err);
+      (void)hipFree(g_cws.buf);
+    }
     g_cws.buf = nullptr;
     g_cws.bytes = 0;
     g_cws.qp_count = -1;
     if ((e = hipMalloc(&g_cws.buf, off)) != hipSuccess) return fail("hipMalloc", e, err);
     g_cws.bytes = off;
-    g_cws.device = dev;
   }
   char* b = static_cast<char*>(g_cws.buf);
   Work W;
@@ -628,15 +633,15 @@ int run_cycle(const Plan& P, int64_t K, const float* Bcumul_host, float* torques
     const int rc = qpgpu_solve_batched_eq(&d, G, g0, CE, ce0, CI, ci0, x1, f1, s1, nullptr, x2,
                                           f2, s2, s);
     if (rc != QPGPU_SUCCESS) {
-      g_cws.err = std::string("qpgpu_solve_batched_eq: ") + qpgpu_last_error();
-      *err = g_cws.err.c_str();
+      g_cws_err = std::string("qpgpu_solve_batched_eq: ") + qpgpu_last_error();
+      *err = g_cws_err.c_str();
       return -3;
     }
     const int acc = l < last ? P.level_row0[l] + p : 0;  // Z after the last level is unused
     const int frc = launch_finish_level(P, W, l, x1, f1, s1, x2, f2, s2, acc, s);
     if (frc == -2) {
-      g_cws.err = "stacked task rows too large for the LDS projector";
-      *err = g_cws.err.c_str();
+      g_cws_err = "stacked task rows too large for the LDS projector";
+      *err = g_cws_err.c_str();
       return -2;
     }
     if (frc) return fail("finish_level", hipGetLastError(), err);

@@ -7,6 +7,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 
@@ -68,28 +69,27 @@ struct HostWorkspace {
 };
 thread_local HostWorkspace g_ws;
 
-// Device workspace for the kernels that keep J and R in global memory (n > 64).  Grow-only,
-// one per device, shared by all threads (serialised by a mutex; kernels on different streams
-// must not overlap on it — documented in include/qpgpu.h).
+// Device workspace for the kernels that keep J and R in global memory (n > 64).  Grow-only and
+// cached per (device, stream), so launches on different streams never share one; growing syncs
+// only the stream that used the old buffer.
 struct DevWorkspace {
   void* buf = nullptr;
   size_t bytes = 0;
 };
 std::mutex g_dev_ws_mu;
-DevWorkspace g_dev_ws[64];
+std::map<std::pair<int, hipStream_t>, DevWorkspace> g_dev_ws;
 
-int device_workspace(int64_t bytes, double** out) {
+int device_workspace(int64_t bytes, hipStream_t stream, double** out) {
   *out = nullptr;
   if (bytes <= 0) return QPGPU_SUCCESS;
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
-  if (dev < 0 || dev >= 64) return QPGPU_ERR_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(g_dev_ws_mu);
-  DevWorkspace& w = g_dev_ws[dev];
+  DevWorkspace& w = g_dev_ws[{dev, stream}];
   if (w.bytes < (size_t)bytes) {
     if (w.buf) {
-      if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+      if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
       (void)hipFree(w.buf);
       w.buf = nullptr;
       w.bytes = 0;
@@ -200,7 +200,7 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
     a.flags |= qpk::kArgAligned16;
   auto launch_wave = [&]() -> int {
     double* ws = nullptr;
-    const int wrc = device_workspace(qpk_medium_workspace_bytes(a.n, a.m, a.batch), &ws);
+    const int wrc = device_workspace(qpk_medium_workspace_bytes(a.n, a.m, a.batch), s, &ws);
     if (wrc) return wrc;
     e = qpk_launch_medium_ws(&a, s, &handled, nullptr, ws);
     return QPGPU_SUCCESS;
