@@ -25,7 +25,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libqpgpu.so")
+LIB_PATH = os.environ.get("QPGPU_LIB_PATH") or os.path.join(LIB_DIR, "libqpgpu.so")  # env: A/B builds only
 DROPIN_PATH = os.path.join(LIB_DIR, "libquadprog_amd.so")
 
 # per-QP status codes (include/qpgpu.h)
