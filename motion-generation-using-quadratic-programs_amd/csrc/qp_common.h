@@ -78,7 +78,7 @@ struct QpArgs {
   // boundaries, kStampSlots per wave, written by lane 0.  Never feeds an output.
   uint64_t* stamps;
 };
-constexpr int kStampSlots = 8;
+constexpr int kStampSlots = 16;
 // internal QpArgs.flags bit set by the host when CI and ci0 are 16-byte aligned
 constexpr uint32_t kArgAligned16 = 0x80000000u;
 

@@ -26,6 +26,68 @@ __device__ __forceinline__ void grp_sync() {
     sg_sync();
 }
 
+// Sequential sums over runtime-length index ranges with the operand loads batched kU at a time:
+// all kU loads of a chunk are issued before the chunk's multiply-adds, so a loop over global
+// (or LDS) operands costs one memory latency per chunk instead of one per element.  The adds
+// stay strictly sequential in the reference's index order, so results are bit-identical.
+// Chunk sizes: operands in global memory (CI always; J and R with GJR) batch kUG loads per
+// chunk; LDS-resident operands use plain sequential loops (kUL = 1).
+constexpr int kUG = 8, kUL = 1;
+
+// s + sum_{j=j0}^{j1-1} A(j) * B(j), j ascending (s += a*b per element)
+template <int kU, class FA, class FB>
+__device__ __forceinline__ double seq_fma_up(double s, int j0, int j1, FA A, FB B) {
+  for (int jb = j0; jb < j1; jb += kU) {
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int j = jb + u;
+      va[u] = j < j1 ? A(j) : 0.0;
+      vb[u] = j < j1 ? B(j) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++)
+      if (jb + u < j1) s += va[u] * vb[u];
+  }
+  return s;
+}
+
+// s - sum A(j) * B(j), j ascending (s -= a*b per element)
+template <int kU, class FA, class FB>
+__device__ __forceinline__ double seq_fms_up(double s, int j0, int j1, FA A, FB B) {
+  for (int jb = j0; jb < j1; jb += kU) {
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int j = jb + u;
+      va[u] = j < j1 ? A(j) : 0.0;
+      vb[u] = j < j1 ? B(j) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++)
+      if (jb + u < j1) s -= va[u] * vb[u];
+  }
+  return s;
+}
+
+// s - sum A(k) * B(k), k DEscending from k1-1 down to k0 (s -= a*b per element)
+template <int kU, class FA, class FB>
+__device__ __forceinline__ double seq_fms_down(double s, int k0, int k1, FA A, FB B) {
+  for (int kb = k1 - 1; kb >= k0; kb -= kU) {
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int k = kb - u;
+      va[u] = k >= k0 ? A(k) : 0.0;
+      vb[u] = k >= k0 ? B(k) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++)
+      if (kb - u >= k0) s -= va[u] * vb[u];
+  }
+  return s;
+}
+
 // per-QP control block (lead lane writes, subgroup reads after grp_sync)
 struct Ctl {
   double f, t, t1, t2, ss, R_norm, c1, c2, psi, ci0ip, znp;
@@ -114,6 +176,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
 #define R_(i, j) Rm[(i) * JS + (j)]
 
   // ------------------------------------------------------------------ setup
+  qp_stamp(a, 0);
   // G -> R region (becomes L), g0 -> z region
   if (live) {
     for (int e = ls; e < n * n; e += S) {
@@ -139,8 +202,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
     // cholesky_decomposition (@.text+0x2df0): row-wise, descending-k sums, upper mirrored.
     for (int i = 0; i < n; i++) {
       if (lead) {
-        double sum = R_(i, i);
-        for (int k = i - 1; k >= 0; k--) sum -= R_(i, k) * R_(i, k);
+        const double sum = seq_fms_down<GJR ? kUG : kUL>(R_(i, i), 0, i, [&](int k) { return R_(i, k); },
+                                        [&](int k) { return R_(i, k); });
         if (sum <= 0.0) {
           ctl->status = QPGPU_QP_NOT_POSITIVE_DEFINITE;
           ctl->f = sum;
@@ -152,8 +215,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
       if (ctl->status != QPGPU_QP_OK) break;
       const double dg = ctl->t;
       for (int j = i + 1 + ls; j < n; j += S) {
-        double s2 = R_(i, j);
-        for (int k = i - 1; k >= 0; k--) s2 -= R_(i, k) * R_(j, k);
+        const double s2 = seq_fms_down<GJR ? kUG : kUL>(R_(i, j), 0, i, [&](int k) { return R_(i, k); },
+                                       [&](int k) { return R_(j, k); });
         R_(j, i) = s2 / dg;
       }
       if (lead) R_(i, i) = dg;
@@ -162,6 +225,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
       grp_sync<S>();
     }
   }
+  qp_stamp(a, 1);
   const bool chol_ok = live && ctl->status == QPGPU_QP_OK;
   if (live && (a.flags & QPGPU_FLAG_WRITE_FACTOR)) {
     double* Gw = a.G + qbase_rt(bb, n * n, T);
@@ -187,8 +251,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
       const int i0 = skip ? r : 0;
       for (int i = 0; i < i0; i++) J_(r, i) = 0.0;
       for (int i = i0; i < n; i++) {
-        double v = (i == r) ? 1.0 : 0.0;
-        for (int j = i0; j < i; j++) v -= R_(i, j) * J_(r, j);
+        const double v = seq_fms_up<GJR ? kUG : kUL>((i == r) ? 1.0 : 0.0, i0, i, [&](int j) { return R_(i, j); },
+                                    [&](int j) { return J_(r, j); });
         J_(r, i) = v / R_(i, i);
       }
     }
@@ -199,13 +263,13 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
       ctl->c2 = c2;
       // cholesky_solve (@.text+0x31a2): y -> d, x = -G^{-1} g0
       for (int i = 0; i < n; i++) {
-        double v = zv[i];
-        for (int j = 0; j < i; j++) v -= R_(i, j) * dv[j];
+        const double v = seq_fms_up<GJR ? kUG : kUL>(zv[i], 0, i, [&](int j) { return R_(i, j); },
+                                    [&](int j) { return dv[j]; });
         dv[i] = v / R_(i, i);
       }
       for (int i = n - 1; i >= 0; i--) {
-        double v = dv[i];
-        for (int j = i + 1; j < n; j++) v -= R_(i, j) * xv[j];
+        const double v = seq_fms_up<GJR ? kUG : kUL>(dv[i], i + 1, n, [&](int j) { return R_(i, j); },
+                                    [&](int j) { return xv[j]; });
         xv[i] = v / R_(i, i);
       }
       double f = 0.0;
@@ -228,34 +292,27 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
     grp_sync<S>();
   }
 
+  qp_stamp(a, 2);
   // ------------------------------------------------------------------ shared kernels
   // d = J^T np (lane = column, j ascending); z = J[:, iq:] d[iq:] (lane = row)
   auto compute_d_z = [&](int iq) {
-    for (int c = ls; c < n; c += S) {
-      double s = 0.0;
-      for (int j = 0; j < n; j++) s += J_(j, c) * npv[j];
-      dv[c] = s;
-    }
+    for (int c = ls; c < n; c += S)
+      dv[c] = seq_fma_up<GJR ? kUG : kUL>(0.0, 0, n, [&](int j) { return J_(j, c); }, [&](int j) { return npv[j]; });
     grp_sync<S>();
-    for (int r = ls; r < n; r += S) {
-      double z = 0.0;
-      for (int j = iq; j < n; j++) z += J_(r, j) * dv[j];
-      zv[r] = z;
-    }
+    for (int r = ls; r < n; r += S)
+      zv[r] = seq_fma_up<GJR ? kUG : kUL>(0.0, iq, n, [&](int j) { return J_(r, j); }, [&](int j) { return dv[j]; });
     grp_sync<S>();
   };
   // lead: update_r (r = R[:iq,:iq]^{-1} d[:iq])
   auto update_r_lead = [&](int iq) {
     for (int i = iq - 1; i >= 0; i--) {
-      double s = 0.0;
-      for (int j = i + 1; j < iq; j++) s += R_(i, j) * rv[j];
+      const double s = seq_fma_up<GJR ? kUG : kUL>(0.0, i + 1, iq, [&](int j) { return R_(i, j); },
+                                  [&](int j) { return rv[j]; });
       rv[i] = (dv[i] - s) / R_(i, i);
     }
   };
   auto dot_lead = [&](const double* u_, const double* v_) {
-    double s = 0.0;
-    for (int i = 0; i < n; i++) s += u_[i] * v_[i];
-    return s;
+    return seq_fma_up<kUL>(0.0, 0, n, [&](int i) { return u_[i]; }, [&](int i) { return v_[i]; });
   };
   // add_constraint (@.text+0x21fd), split: the lead runs the d-chain and records each Givens
   // coefficient set (gc, gs, gx; gx = NaN marks a skipped |h| < eps step), every lane then
@@ -466,9 +523,13 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
     }
   }
 
+  qp_stamp(a, 3);
   // ------------------------------------------------------------------ active-set loop
   // Per-subgroup state machine; a wave loops until all of its QPs are done.
   const int max_steps = a.max_steps;
+  // diagnostic phase clocks (stamps only): scan, select, d/z, lead step, add, delete
+  uint64_t tph[6] = {0, 0, 0, 0, 0, 0};
+  auto clk = [&]() -> uint64_t { return a.stamps ? __builtin_amdgcn_s_memtime() : 0; };
   while (true) {
     const int phase = ctl->phase;
     if (S < 64) {
@@ -478,15 +539,17 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
     }
     if (phase == PH_DONE) continue;  // other subgroups of this wave are still busy
     if (phase == PH_SCAN) {
+      const uint64_t t0 = clk();
       // ---- l1
       if (lead) {
         ctl->iter++;
         for (int i = p; i < ctl->iq; i++) act[Av[i]] = 1;
       }
       for (int i = ls; i < m; i += S) {
-        double s = 0.0;
-        for (int j = 0; j < n; j++) s += EL(CIb, j * m + i) * xv[j];
-        s += EL(ci0b, i);
+        const double c0 = EL(ci0b, i);  // issued with the first chunk, added last
+        double s = seq_fma_up<kUG>(0.0, 0, n, [&](int j) { return EL(CIb, j * m + i); },
+                              [&](int j) { return xv[j]; });
+        s += c0;
         sv[i] = s;
         exc[i] = 0;
       }
@@ -508,9 +571,11 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
       }
       for (int i = ls; i < n; i += S) xo[i] = xv[i];
       grp_sync<S>();
+      tph[0] += clk() - t0;
       continue;
     }
     if (phase == PH_SELECT) {
+      const uint64_t t0 = clk();
       // ---- l2 (ss deliberately not reset: reference quirk)
       if (lead) {
         double ss = ctl->ss;
@@ -537,6 +602,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
         for (int j = ls; j < n; j += S) npv[j] = EL(CIb, j * m + ip);
         grp_sync<S>();
       }
+      tph[1] += clk() - t0;
       continue;
     }
     // ---- l2a (phase == PH_STEP)
@@ -548,7 +614,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
     }
     grp_sync<S>();
     if (ctl->phase == PH_DONE) continue;
+    uint64_t t0 = clk();
     compute_d_z(ctl->iq);
+    uint64_t t1c = clk();
+    tph[2] += t1c - t0;
     int kind = 0;  // 1 infeasible, 2 dual step, 3 full step, 4 partial step
     if (lead) {
       const int iq = ctl->iq;
@@ -594,9 +663,12 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
     }
     grp_sync<S>();
     kind = ctl->qq;
+    t0 = clk();
+    tph[3] += t0 - t1c;
     if (kind == 1) continue;
     if (kind == 2) {
       delete_constraint(ctl->l);
+      tph[5] += clk() - t0;
       if (lead) ctl->phase = PH_STEP;
       grp_sync<S>();
       continue;
@@ -607,7 +679,9 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
     }
     grp_sync<S>();
     if (kind == 3) {
+      const uint64_t ta = clk();
       add_constraint();
+      tph[4] += clk() - ta;
       if (!ctl->fin) {
         const int ip = ctl->ip;
         if (lead) exc[ip] = 1;
@@ -635,10 +709,14 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
     // partial step: drop l, refresh s[ip]
     if (lead) act[ctl->l] = 0;
     grp_sync<S>();
-    delete_constraint(ctl->l);
+    {
+      const uint64_t td = clk();
+      delete_constraint(ctl->l);
+      tph[5] += clk() - td;
+    }
     if (lead) {
-      double s = 0.0;
-      for (int k = 0; k < n; k++) s += npv[k] * xv[k];
+      const double s = seq_fma_up<kUL>(0.0, 0, n, [&](int k) { return npv[k]; },
+                                  [&](int k) { return xv[k]; });
       sv[ctl->ip] = s + ctl->ci0ip;
       ctl->phase = PH_STEP;
     }
@@ -647,6 +725,9 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
 #undef J_
 #undef R_
 
+  qp_stamp(a, 4);
+  if (a.stamps && threadIdx.x == 0)
+    for (int k = 0; k < 6; k++) a.stamps[(uint64_t)blockIdx.x * kStampSlots + 8 + k] = tph[k];
   // ------------------------------------------------------------------ outputs
   if (live) {
     const int st = ctl->status;

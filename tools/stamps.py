@@ -21,7 +21,7 @@ B = 65536
 pr = qpgpu.make_problems(kind, n, p, m, 0, B, seed=2026)
 db = qpgpu.DeviceBatch(pr, "cuda:0", layout=layout)
 waves = (B + 63) // 64
-st = torch.zeros(waves * 8, dtype=torch.int64, device="cuda:0")
+st = torch.zeros(waves * 16, dtype=torch.int64, device="cuda:0")
 fn = qpgpu.LIB.qpgpu_debug_set_stamps
 fn.argtypes = [ctypes.c_void_p]
 for rep in range(3):
@@ -29,7 +29,7 @@ for rep in range(3):
     db.solve(family="lane")
     torch.cuda.synchronize()
 fn(None)
-s = st.cpu().numpy().reshape(waves, 8).astype(np.int64)
+s = st.cpu().numpy().reshape(waves, 16).astype(np.int64)
 it = db.iters.cpu().numpy()[: waves * 64].reshape(waves, 64)
 names = ["loads+setup", "equality", "active-set", "stores"]
 tot = s[:, 4] - s[:, 0]
