@@ -86,6 +86,14 @@ enum qpgpu_error {
                                           reference does (QuadProg++.hh:42-45).  Off by default
                                           in batched use: it is extra HBM traffic. */
 
+#define QPGPU_FLAG_EXACT 0x2u         /* keep the reference's floating-point operation order
+                                          everywhere, so x and f are bit-identical to QuadProg++.
+                                          Shapes up to n = 64 always do; for n > 64 the default
+                                          runs the O(n^3) setup (Cholesky, J = L^-T, x0) as
+                                          blocked f64 MFMA (qp_panel.hip), which matches the
+                                          reference within 1e-10 relative instead.  Implied by
+                                          QPGPU_FLAG_WRITE_FACTOR. */
+
 /* Kernel-family selection (benchmarking / testing knobs; default = fastest for the shape):
  *   LANE      one QP per lane (qp_lane.hip, n <= 8, m <= 16)
  *   SUBGROUP  one QP per S-lane subgroup, register state (qp_small.hip, n <= 16, m <= 64)

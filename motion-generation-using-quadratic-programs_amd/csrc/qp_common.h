@@ -81,6 +81,23 @@ struct QpArgs {
 constexpr int kStampSlots = 16;
 // internal QpArgs.flags bit set by the host when CI and ci0 are 16-byte aligned
 constexpr uint32_t kArgAligned16 = 0x80000000u;
+// internal QpArgs.flags bit: the workspace already holds the setup (qp_panel.hip) — J, x0, f0,
+// c1, c2 and the Cholesky status — so the loop kernel starts at the equality phase
+constexpr uint32_t kSetupDone = 0x40000000u;
+
+// Per-QP device workspace of the large-QP path (n > 64, qp_wave.hip GJR + qp_panel.hip):
+//   [0, OFF_R)        J, COLUMN-major: J[k][j] at j*JS + k
+//   [OFF_R, OFF_H)    R row-major (R[i][j] at i*JS + j); the setup's scratch for G -> L
+//   [OFF_H, PER_QP)   header: status, f0, c1, c2, (pad), x0 at HX
+constexpr int kBigN = 256;
+template <int NMAX>
+struct BigWs {
+  static constexpr int JS = NMAX + 1;
+  static constexpr int64_t OFF_R = (int64_t)NMAX * JS;
+  static constexpr int64_t OFF_H = 2 * (int64_t)NMAX * JS;
+  static constexpr int HX = 8;
+  static constexpr int64_t PER_QP = OFF_H + HX + NMAX;
+};
 
 __device__ __forceinline__ void qp_stamp(const QpArgs& a, int slot) {
   if (a.stamps) {

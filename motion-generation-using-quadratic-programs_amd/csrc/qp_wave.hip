@@ -123,7 +123,8 @@ struct WaveCfg {
   static constexpr int PER_QP = OFF_CTL + (int)(sizeof(Ctl) / 8);
   static constexpr int STRIDE = PER_QP | 1;
   static constexpr int LDS_DOUBLES = QPB * STRIDE;
-  static constexpr int WS_DOUBLES = GJR ? 2 * NMAX * JS : 0;  // per QP, global workspace
+  static_assert(!GJR || JS == BigWs<NMAX>::JS, "workspace layout shared with qp_panel.hip");
+  static constexpr int64_t WS_DOUBLES = GJR ? BigWs<NMAX>::PER_QP : 0;  // per QP, global workspace
 };
 
 template <int S, int NMAX, int MMAX, bool GJR>
@@ -172,20 +173,42 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
   const double* CIb = a.CI + qbase_rt(bb, n * m, T);
   const double* ci0b = a.ci0 + qbase_rt(bb, m, T);
 #define EL(ptr, e) (ptr)[(int64_t)(e) * T]
-#define J_(i, j) Jm[(i) * JS + (j)]
+  // J in LDS: row-major.  J in the workspace (GJR): column-major, so that the row-parallel work
+  // (Givens sweeps, update_z, building J) reads and writes it coalesced across lanes.
+#define J_(i, j) (GJR ? Jm[(j) * JS + (i)] : Jm[(i) * JS + (j)])
 #define R_(i, j) Rm[(i) * JS + (j)]
+  // setup already in the workspace (qp_panel.hip): start from its header
+  const bool pre = GJR && (a.flags & kSetupDone);
 
   // ------------------------------------------------------------------ setup
   qp_stamp(a, 0);
+  if (pre) {
+    const double* H = Jm + BigWs<NMAX>::OFF_H;
+    if (lead) {
+      ctl->iter = 0;
+      ctl->steps = 0;
+      ctl->fin = 1;
+      ctl->status = live ? (int)H[0] : QPGPU_QP_OK;
+      ctl->f = H[1];
+      ctl->c1 = H[2];
+      ctl->c2 = H[3];
+      ctl->R_norm = 1.0;
+      ctl->iq = 0;
+      ctl->phase = live ? PH_SCAN : PH_DONE;
+    }
+    if (live)
+      for (int i = ls; i < n; i += S) xv[i] = H[BigWs<NMAX>::HX + i];
+    grp_sync<S>();
+  }
   // G -> R region (becomes L), g0 -> z region
-  if (live) {
+  if (live && !pre) {
     for (int e = ls; e < n * n; e += S) {
       const int i = e / n, j = e - (e / n) * n;
       R_(i, j) = EL(Gb, e);
     }
     for (int i = ls; i < n; i += S) zv[i] = EL(g0b, i);
   }
-  if (lead) {
+  if (lead && !pre) {
     ctl->status = QPGPU_QP_OK;
     ctl->iter = 0;
     ctl->steps = 0;
@@ -193,7 +216,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
     ctl->fin = 1;
   }
   grp_sync<S>();
-  if (live) {
+  if (live && !pre) {
     if (lead) {
       double c1 = 0.0;
       for (int i = 0; i < n; i++) c1 += R_(i, i);
@@ -227,11 +250,11 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
   }
   qp_stamp(a, 1);
   const bool chol_ok = live && ctl->status == QPGPU_QP_OK;
-  if (live && (a.flags & QPGPU_FLAG_WRITE_FACTOR)) {
+  if (live && !pre && (a.flags & QPGPU_FLAG_WRITE_FACTOR)) {
     double* Gw = a.G + qbase_rt(bb, n * n, T);
     for (int e = ls; e < n * n; e += S) EL(Gw, e) = R_(e / n, e - (e / n) * n);
   }
-  if (chol_ok) {
+  if (chol_ok && !pre) {
     // J = L^{-T}: lane r builds row r = (L^{-1} e_r)^T in place (J_(r, .) is its own scratch).
     // With a finite L the first r entries are exactly +0.0 and add exact zeros later: skipped
     // (same bits).  A non-finite L takes the literal path.
@@ -282,6 +305,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
       ctl->iq = 0;
     }
     grp_sync<S>();
+  }
+  if (chol_ok) {
     // R = 0 (L no longer needed), flags
     for (int e = ls; e < n * JS; e += S) Rm[e] = 0.0;
     for (int i = ls; i < m; i += S) act[i] = exc[i] = 0;
@@ -352,18 +377,34 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
     grp_sync<S>();
     const int iq0 = ctl->iq;
     if (iq0 < n) {
+      // Row k's sweep over columns n-1 .. iq: rotation g maps (J[k][j-1], J[k][j]), j = n-1-g,
+      // to (n1, xny (t1 + n1) - t2) and n1 is the next rotation's t2, so it is carried in a
+      // register and the t1 loads (independent of the chain) are issued kU at a time.
+      constexpr int kU = GJR ? kUG : 2;
       const int ng = ctl->ngiv;
       for (int k = ls; k < n; k += S) {
-        for (int g = 0; g < ng; g++) {
-          if (gf[g] == 0.0) continue;  // skipped step
-          const double xny = gx[g];
-          const int j = n - 1 - g;
-          const double cc = gc[g], ss = gs[g];
-          const double t1 = J_(k, j - 1), t2 = J_(k, j);
-          const double n1 = t1 * cc + t2 * ss;
-          J_(k, j - 1) = n1;
-          J_(k, j) = xny * (t1 + n1) - t2;
+        double carry = J_(k, n - 1);
+        for (int gb = 0; gb < ng; gb += kU) {
+          double t1v[kU];
+#pragma unroll
+          for (int u = 0; u < kU; u++) t1v[u] = (gb + u < ng) ? J_(k, n - 2 - gb - u) : 0.0;
+#pragma unroll
+          for (int u = 0; u < kU; u++) {
+            const int g = gb + u;
+            if (g < ng) {
+              const double t1 = t1v[u], t2 = carry;
+              if (gf[g] != 0.0) {
+                const double n1 = t1 * gc[g] + t2 * gs[g];
+                J_(k, n - 1 - g) = gx[g] * (t1 + n1) - t2;
+                carry = n1;
+              } else {  // skipped step: both columns unchanged
+                J_(k, n - 1 - g) = t2;
+                carry = t1;
+              }
+            }
+          }
         }
+        J_(k, n - 1 - ng) = carry;
       }
     }
     grp_sync<S>();
@@ -456,18 +497,33 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
     }
     grp_sync<S>();
     {
+      // row k's sweep over columns qq .. qq+ng: rotation g maps (J[k][j], J[k][j+1]), j = qq+g,
+      // to (n1, xny (n1 + t1) - t2); the second is the next rotation's t1 (carried)
+      constexpr int kU = GJR ? kUG : 2;
       const int ng = ctl->ngiv, qq = ctl->qq;
       for (int k = ls; k < n; k += S) {
-        for (int g = 0; g < ng; g++) {
-          if (gf[g] == 0.0) continue;
-          const double xny = gx[g];
-          const int j = qq + g;
-          const double cc = gc[g], ss = gs[g];
-          const double t1 = J_(k, j), t2 = J_(k, j + 1);
-          const double n1 = t1 * cc + t2 * ss;
-          J_(k, j) = n1;
-          J_(k, j + 1) = xny * (n1 + t1) - t2;
+        double carry = J_(k, qq);
+        for (int gb = 0; gb < ng; gb += kU) {
+          double t2v[kU];
+#pragma unroll
+          for (int u = 0; u < kU; u++) t2v[u] = (gb + u < ng) ? J_(k, qq + gb + u + 1) : 0.0;
+#pragma unroll
+          for (int u = 0; u < kU; u++) {
+            const int g = gb + u;
+            if (g < ng) {
+              const double t1 = carry, t2 = t2v[u];
+              if (gf[g] != 0.0) {
+                const double n1 = t1 * gc[g] + t2 * gs[g];
+                J_(k, qq + g) = n1;
+                carry = gx[g] * (n1 + t1) - t2;
+              } else {
+                J_(k, qq + g) = t1;
+                carry = t2;
+              }
+            }
+          }
         }
+        J_(k, qq + ng) = carry;
       }
     }
     grp_sync<S>();
@@ -766,7 +822,8 @@ static const WaveVariant kWaveVariants[] = {
     {32, 128, 0, "qp_wave<S=32,N=32,M=128>", launch_wave<32, 32, 128, false>},
     {64, 128, 0, "qp_wave<S=64,N=64,M=128>", launch_wave<64, 64, 128, false>},
     {64, 256, 0, "qp_wave<S=64,N=64,M=256>", launch_wave<64, 64, 256, false>},
-    {256, 1024, WaveCfg<256, 256, 1024, true>::WS_DOUBLES, "qp_wave<S=256,N=256,M=1024,global J/R>",
+    {256, 1024, WaveCfg<256, 256, 1024, true>::WS_DOUBLES,
+     "qp_panel<MFMA f64 16x16x4> + qp_wave<S=256,N=256,M=1024,global J/R>",
      launch_wave<256, 256, 1024, true>},
 };
 
@@ -789,6 +846,15 @@ extern "C" int64_t qpk_medium_workspace_bytes(int n, int m, int64_t batch) {
   const qpk::WaveVariant* v = qpk::pick_wave(n, m);
   return v ? v->ws_doubles_per_qp * 8 * batch : 0;
 }
+extern "C" hipError_t qpk_launch_panel_setup(const qpk::QpArgs* a, hipStream_t stream, double* ws);
+
+// Workspace variants (n > 64) run the MFMA panel setup (qp_panel.hip) first unless the caller
+// asked for the reference's exact operation order (QPGPU_FLAG_EXACT) or for the factor in G
+// (QPGPU_FLAG_WRITE_FACTOR: the reference's bits), which the serial restatement here provides.
+static bool uses_panel(const qpk::WaveVariant* v, uint32_t flags) {
+  return v->ws_doubles_per_qp > 0 && !(flags & (QPGPU_FLAG_EXACT | QPGPU_FLAG_WRITE_FACTOR));
+}
+
 extern "C" hipError_t qpk_launch_medium_ws(const qpk::QpArgs* a, hipStream_t stream, int* handled,
                                           const char** name, double* ws) {
   const qpk::WaveVariant* v = qpk::pick_wave(a->n, a->m);
@@ -798,5 +864,12 @@ extern "C" hipError_t qpk_launch_medium_ws(const qpk::QpArgs* a, hipStream_t str
   }
   *handled = 1;
   if (name) *name = v->name;
+  if (uses_panel(v, a->flags)) {
+    hipError_t e = qpk_launch_panel_setup(a, stream, ws);
+    if (e != hipSuccess) return e;
+    qpk::QpArgs b = *a;
+    b.flags |= qpk::kSetupDone;
+    return v->launch(b, stream, ws);
+  }
   return v->launch(*a, stream, ws);
 }

@@ -50,7 +50,7 @@ int validate(const qpgpu_problem_desc* d) {
   if (d->layout != QPGPU_LAYOUT_QP_MAJOR && d->layout != QPGPU_LAYOUT_TILED64)
     return QPGPU_ERR_INVALID_ARGUMENT;
   const uint32_t fam = QPGPU_FLAG_FORCE_LANE | QPGPU_FLAG_FORCE_SUBGROUP | QPGPU_FLAG_FORCE_WAVE;
-  const uint32_t known = QPGPU_FLAG_WRITE_FACTOR | fam;
+  const uint32_t known = QPGPU_FLAG_WRITE_FACTOR | QPGPU_FLAG_EXACT | fam;
   if (d->flags & ~known) return QPGPU_ERR_INVALID_ARGUMENT;
   const uint32_t f = d->flags & fam;
   if (f & (f - 1)) return QPGPU_ERR_INVALID_ARGUMENT;  // at most one family
@@ -195,7 +195,7 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int handled = 0;
   hipError_t e = hipSuccess;
-  a.flags = d->flags & QPGPU_FLAG_WRITE_FACTOR;
+  a.flags = d->flags & (QPGPU_FLAG_WRITE_FACTOR | QPGPU_FLAG_EXACT);
   if (((reinterpret_cast<uintptr_t>(CI) | reinterpret_cast<uintptr_t>(ci0)) & 15u) == 0)
     a.flags |= qpk::kArgAligned16;
   auto launch_wave = [&]() -> int {

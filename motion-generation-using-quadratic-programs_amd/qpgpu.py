@@ -44,6 +44,7 @@ ERR_HIP = 3
 ERR_NO_DEVICE = 4
 
 FLAG_WRITE_FACTOR = 0x1
+FLAG_EXACT = 0x2  # reference operation order for n > 64 too (no MFMA panel setup)
 FLAG_FORCE_LANE = 0x100
 FLAG_FORCE_SUBGROUP = 0x200
 FLAG_FORCE_WAVE = 0x400
@@ -186,13 +187,15 @@ def algorithmic_bytes_per_qp(n: int, p: int, m: int) -> int:
 # host-pointer solve (numpy in, numpy out) — copies through the C-ABI's host entry point
 # ----------------------------------------------------------------------------------------------
 def solve_batched_host(pr: Problems, write_factor: bool = False, max_iter: int = 0, family=None,
-                       layout=None):
+                       layout=None, exact: bool = False):
     """Solve every QP of `pr` on the GPU.  Returns (x, f, status, iters).
 
     With write_factor=True, pr.G is overwritten with each QP's Cholesky factor, as the
     reference overwrites G (QuadProg++.hh:42-45).  layout="tiled64" sends the batch in the
-    TILED64 layout (converted here on the host) and converts x / G back."""
+    TILED64 layout (converted here on the host) and converts x / G back.  exact=True keeps the
+    reference's operation order for n > 64 as well (QPGPU_FLAG_EXACT)."""
     B, n, p, m = pr.batch, pr.n, pr.p, pr.m
+    xflags = FAMILY_FLAGS[family] | (FLAG_EXACT if exact else 0)
     if LAYOUTS[layout] == LAYOUT_TILED64:
         arrs = [to_tiled64(np.asarray(a, dtype=np.float64)) for a in pr.arrays()]
         xt = np.zeros((B + 63) // 64 * 64 * n, dtype=np.float64)
@@ -200,7 +203,7 @@ def solve_batched_host(pr: Problems, write_factor: bool = False, max_iter: int =
         st = np.zeros(B, dtype=np.int32)
         it = np.zeros(B, dtype=np.int32)
         d = ProblemDesc(n, p, m, max_iter, B,
-                        (FLAG_WRITE_FACTOR if write_factor else 0) | FAMILY_FLAGS[family], LAYOUT_TILED64)
+                        (FLAG_WRITE_FACTOR if write_factor else 0) | xflags, LAYOUT_TILED64)
         rc = LIB.qpgpu_solve_batched_host(ctypes.byref(d), *[_ptr(a) for a in arrs], _ptr(xt), _ptr(f),
                                           _ptr(st), _ptr(it))
         _check(rc, "qpgpu_solve_batched_host")
@@ -216,7 +219,7 @@ def solve_batched_host(pr: Problems, write_factor: bool = False, max_iter: int =
     f = np.zeros(B, dtype=np.float64)
     st = np.zeros(B, dtype=np.int32)
     it = np.zeros(B, dtype=np.int32)
-    d = ProblemDesc(n, p, m, max_iter, B, (FLAG_WRITE_FACTOR if write_factor else 0) | FAMILY_FLAGS[family], 0)
+    d = ProblemDesc(n, p, m, max_iter, B, (FLAG_WRITE_FACTOR if write_factor else 0) | xflags, 0)
     rc = LIB.qpgpu_solve_batched_host(ctypes.byref(d), *[_ptr(a) for a in arrs], _ptr(x), _ptr(f),
                                       _ptr(st), _ptr(it))
     _check(rc, "qpgpu_solve_batched_host")
@@ -244,7 +247,7 @@ class DeviceBatch:
         self.iters = torch.zeros(self.batch, dtype=torch.int32, device=device) if with_iters else None
 
     def solve(self, stream=None, max_iter: int = 0, write_factor: bool = False, family=None,
-              eq_out=None):
+              eq_out=None, exact: bool = False):
         """Enqueue one batched solve on `stream` (a torch.cuda.Stream, default current).
         eq_out=(x_eq, f_eq, status_eq) tensors also receive the m = 0 answer
         (qpgpu_solve_batched_eq)."""
@@ -253,7 +256,8 @@ class DeviceBatch:
         if stream is None:
             stream = torch.cuda.current_stream(self.x.device)
         d = ProblemDesc(self.n, self.p, self.m, max_iter, self.batch,
-                        (FLAG_WRITE_FACTOR if write_factor else 0) | FAMILY_FLAGS[family], self.layout)
+                        (FLAG_WRITE_FACTOR if write_factor else 0) | FAMILY_FLAGS[family]
+                        | (FLAG_EXACT if exact else 0), self.layout)
         vp = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
         args = [ctypes.byref(d), vp(self.G), vp(self.g0), vp(self.CE), vp(self.ce0), vp(self.CI),
                 vp(self.ci0), vp(self.x), vp(self.f), vp(self.status), vp(self.iters)]
@@ -264,11 +268,11 @@ class DeviceBatch:
                                             ctypes.c_void_p(stream.cuda_stream))
         _check(rc, "qpgpu_solve_batched")
 
-    def launcher(self, stream, max_iter: int = 0, family=None):
+    def launcher(self, stream, max_iter: int = 0, family=None, exact: bool = False):
         """A zero-argument callable that enqueues this batch's solve on `stream` with every ctypes
         argument prebuilt (for tight launch loops: ~2 us of host time per launch)."""
-        d = ProblemDesc(self.n, self.p, self.m, max_iter, self.batch, FAMILY_FLAGS[family],
-                        self.layout)
+        d = ProblemDesc(self.n, self.p, self.m, max_iter, self.batch,
+                        FAMILY_FLAGS[family] | (FLAG_EXACT if exact else 0), self.layout)
         vp = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
         args = (ctypes.byref(d), vp(self.G), vp(self.g0), vp(self.CE), vp(self.ce0), vp(self.CI),
                 vp(self.ci0), vp(self.x), vp(self.f), vp(self.status), vp(self.iters),
