@@ -132,6 +132,9 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
     qp_wave_kernel(const QpArgs a, double* __restrict__ ws) {
   using C = WaveCfg<S, NMAX, MMAX, GJR>;
   constexpr int JS = C::JS;
+  // loads in flight per lane in the global-operand sums (deeper for the one-QP-per-workgroup
+  // workspace variant, whose lanes have registers to spare)
+  constexpr int KG = GJR ? 16 : kUG;
   __shared__ double lds[C::LDS_DOUBLES];
 
   const int tid = threadIdx.x;
@@ -322,57 +325,144 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
   // d = J^T np (lane = column, j ascending); z = J[:, iq:] d[iq:] (lane = row)
   auto compute_d_z = [&](int iq) {
     for (int c = ls; c < n; c += S)
-      dv[c] = seq_fma_up<GJR ? kUG : kUL>(0.0, 0, n, [&](int j) { return J_(j, c); }, [&](int j) { return npv[j]; });
+      dv[c] = seq_fma_up<GJR ? KG : kUL>(0.0, 0, n, [&](int j) { return J_(j, c); }, [&](int j) { return npv[j]; });
     grp_sync<S>();
     for (int r = ls; r < n; r += S)
-      zv[r] = seq_fma_up<GJR ? kUG : kUL>(0.0, iq, n, [&](int j) { return J_(r, j); }, [&](int j) { return dv[j]; });
+      zv[r] = seq_fma_up<GJR ? KG : kUL>(0.0, iq, n, [&](int j) { return J_(r, j); }, [&](int j) { return dv[j]; });
     grp_sync<S>();
   };
-  // lead: update_r (r = R[:iq,:iq]^{-1} d[:iq])
-  auto update_r_lead = [&](int iq) {
-    for (int i = iq - 1; i >= 0; i--) {
-      const double s = seq_fma_up<GJR ? kUG : kUL>(0.0, i + 1, iq, [&](int j) { return R_(i, j); },
-                                  [&](int j) { return rv[j]; });
-      rv[i] = (dv[i] - s) / R_(i, i);
+  // update_r (r = R[:iq,:iq]^{-1} d[:iq], rows i descending, each s = sum_{j>i} R[i][j] r[j]
+  // with j ascending).  LDS-resident R: the lead alone.  R in the workspace (GJR): wave 0 works
+  // as the lead's load/multiply unit — its lanes hold row i-1's R entries (loaded while row i is
+  // summed) and, once r[i] is known, write the products R[i][j] r[j] (the same single rounding
+  // as the reference's `R[i][j] * r[j]`) to LDS; the lead then adds them in j order.  Called by
+  // every lane of the subgroup.
+  auto update_r = [&](int iq) {
+    if constexpr (!GJR) {
+      if (lead)
+        for (int i = iq - 1; i >= 0; i--) {
+          const double s = seq_fma_up<kUL>(0.0, i + 1, iq, [&](int j) { return R_(i, j); },
+                                      [&](int j) { return rv[j]; });
+          rv[i] = (dv[i] - s) / R_(i, i);
+        }
+    } else {
+      if (ls >= 64) return;  // waves 1.. idle (they wait at the caller's grp_sync)
+      constexpr int PU = (NMAX + 63) / 64;
+      double* const P = gc;  // scratch (the Givens buffers are free during a step)
+      double rn[PU], rc[PU];
+      auto fetch = [&](int i) {
+#pragma unroll
+        for (int u = 0; u < PU; u++) {
+          const int j = i + 1 + ls + 64 * u;
+          rn[u] = (i >= 0 && j < iq) ? R_(i, j) : 0.0;
+        }
+      };
+      fetch(iq - 1);
+      for (int i = iq - 1; i >= 0; i--) {
+#pragma unroll
+        for (int u = 0; u < PU; u++) rc[u] = rn[u];
+        fetch(i - 1);  // in flight while row i is finished
+#pragma unroll
+        for (int u = 0; u < PU; u++) {
+          const int j = i + 1 + ls + 64 * u;
+          if (j < iq) P[j] = rc[u] * rv[j];
+        }
+        sg_sync();
+        if (lead) {
+          double s = 0.0;
+          int j = i + 1;
+          for (; j + 4 <= iq; j += 4) {
+            const double p0 = P[j], p1 = P[j + 1], p2 = P[j + 2], p3 = P[j + 3];
+            s += p0;
+            s += p1;
+            s += p2;
+            s += p3;
+          }
+          for (; j < iq; j++) s += P[j];
+          rv[i] = (dv[i] - s) / R_(i, i);
+        }
+        sg_sync();
+      }
     }
+  };
+  // the lead's two step dot products z.z and z.np, one pass (two independent chains)
+  auto dot2_lead = [&](double& zz, double& znp) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = 0; i < n; i++) {
+      const double z = zv[i];
+      s1 += z * z;
+      s2 += z * npv[i];
+    }
+    zz = s1;
+    znp = s2;
   };
   auto dot_lead = [&](const double* u_, const double* v_) {
     return seq_fma_up<kUL>(0.0, 0, n, [&](int i) { return u_[i]; }, [&](int i) { return v_[i]; });
   };
-  // add_constraint (@.text+0x21fd), split: the lead runs the d-chain and records each Givens
-  // coefficient set (gc, gs, gx; gx = NaN marks a skipped |h| < eps step), every lane then
-  // applies the recorded rotations to its rows of J in the same order; the lead finishes with
-  // R[:iq, iq-1] = d and the degeneracy test.  Returns through ctl->fin (1 = added).
-  // gf[g] = 0 marks a step the reference skips (|h| < eps).
+  // add_constraint (@.text+0x21fd), split in three:
+  //  1. the lead runs the serial part of the d-chain.  Rotation g (j = n-1-g) computes
+  //     h = distance(d[j-1], d[j]), and distance() reads magnitudes only, while the rotated d[j-1]
+  //     is +-h; so the chain of h values needs nothing but the previous |h| (or, after a skipped
+  //     |h| < eps step, the untouched d[j-1]).  The lead records h (gx) and applied/skipped (gf);
+  //  2. lane g rebuilds rotation g's inputs exactly as the reference sees them (d[j-1] is still
+  //     the original; d[j] is the original, or +-h of rotation g-1 with the sign of
+  //     d[j] / h_{g-1}) and evaluates the same cc = d[j-1]/h, ss = d[j]/h, sign flip and
+  //     xny = ss/(1+cc) as the reference — every rotation in parallel, bit for bit;
+  //  3. every lane applies the rotations to its rows of J in order; the lead finishes with
+  //     R[:iq, iq-1] = d and the degeneracy test.  Returns through ctl->fin (1 = added).
+  static_assert(S >= NMAX, "one lane per rotation");
   auto add_constraint = [&]() {
     if (lead) {
       const int iq = ctl->iq;
       int ng = 0;
       if (iq < n) {
+        double carried = dv[n - 1];
         for (int j = n - 1; j >= iq + 1; j--) {
-          double cc = dv[j - 1], ss = dv[j];
-          const double h = qp_distance(cc, ss);
-          if (fabs(h) < kEps) {
-            gf[ng++] = 0.0;
-            continue;
-          }
-          dv[j] = 0.0;
-          ss = ss / h;
-          cc = cc / h;
-          if (cc < 0.0) {
-            cc = -cc;
-            ss = -ss;
-            dv[j - 1] = -h;
-          } else {
-            dv[j - 1] = h;
-          }
-          gc[ng] = cc;
-          gs[ng] = ss;
-          gx[ng] = ss / (1.0 + cc);
-          gf[ng++] = 1.0;
+          const double a0 = dv[j - 1];
+          const double h = qp_distance(a0, carried);
+          const bool skip = fabs(h) < kEps;
+          gf[ng] = skip ? 0.0 : 1.0;
+          gx[ng] = h;
+          carried = skip ? a0 : h;
+          ng++;
         }
       }
       ctl->ngiv = ng;
+    }
+    grp_sync<S>();
+    {
+      const int ng = ctl->ngiv, g = ls;
+      const bool mine = g < ng;
+      double cc = 0.0, ss = 0.0, xny = 0.0, dlast = 0.0;
+      if (mine) {
+        const int j = n - 1 - g;
+        const double h = gx[g], cc_raw = dv[j - 1];
+        double ss_raw = dv[j];
+        if (g > 0 && gf[g - 1] != 0.0) {
+          const double hp = gx[g - 1];
+          ss_raw = (dv[j] / hp < 0.0) ? -hp : hp;
+        }
+        dlast = cc_raw;
+        if (gf[g] != 0.0) {
+          ss = ss_raw / h;
+          cc = cc_raw / h;
+          if (cc < 0.0) {
+            cc = -cc;
+            ss = -ss;
+            dlast = -h;
+          } else {
+            dlast = h;
+          }
+          xny = ss / (1.0 + cc);
+        }
+      }
+      grp_sync<S>();
+      if (mine) {
+        gc[g] = cc;
+        gs[g] = ss;
+        gx[g] = xny;
+        if (g == ng - 1) dv[n - 1 - g - 1] = dlast;  // d[iq] after the sweep
+      }
     }
     grp_sync<S>();
     const int iq0 = ctl->iq;
@@ -380,7 +470,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
       // Row k's sweep over columns n-1 .. iq: rotation g maps (J[k][j-1], J[k][j]), j = n-1-g,
       // to (n1, xny (t1 + n1) - t2) and n1 is the next rotation's t2, so it is carried in a
       // register and the t1 loads (independent of the chain) are issued kU at a time.
-      constexpr int kU = GJR ? kUG : 2;
+      constexpr int kU = GJR ? KG : 2;
       const int ng = ctl->ngiv;
       for (int k = ls; k < n; k += S) {
         double carry = J_(k, n - 1);
@@ -499,7 +589,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
     {
       // row k's sweep over columns qq .. qq+ng: rotation g maps (J[k][j], J[k][j+1]), j = qq+g,
       // to (n1, xny (n1 + t1) - t2); the second is the next rotation's t1 (carried)
-      constexpr int kU = GJR ? kUG : 2;
+      constexpr int kU = GJR ? KG : 2;
       const int ng = ctl->ngiv, qq = ctl->qq;
       for (int k = ls; k < n; k += S) {
         double carry = J_(k, qq);
@@ -535,12 +625,11 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
       for (int j = ls; j < n; j += S) npv[j] = EL(CEb, j * p + i);
       grp_sync<S>();
       compute_d_z(ctl->iq);
+      update_r(ctl->iq);
       if (lead) {
         const int iq = ctl->iq;
-        update_r_lead(iq);
-        double t2 = 0.0;
-        const double zz = dot_lead(zv, zv);
-        const double znp = dot_lead(zv, npv);
+        double t2 = 0.0, zz, znp;
+        dot2_lead(zz, znp);
         if (fabs(zz) > kEps) t2 = (-dot_lead(npv, xv) - EL(ce0b, i)) / znp;
         ctl->t2 = t2;
         uv[iq] = t2;
@@ -603,7 +692,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
       }
       for (int i = ls; i < m; i += S) {
         const double c0 = EL(ci0b, i);  // issued with the first chunk, added last
-        double s = seq_fma_up<kUG>(0.0, 0, n, [&](int j) { return EL(CIb, j * m + i); },
+        double s = seq_fma_up<KG>(0.0, 0, n, [&](int j) { return EL(CIb, j * m + i); },
                               [&](int j) { return xv[j]; });
         s += c0;
         sv[i] = s;
@@ -675,9 +764,9 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
     uint64_t t1c = clk();
     tph[2] += t1c - t0;
     int kind = 0;  // 1 infeasible, 2 dual step, 3 full step, 4 partial step
+    update_r(ctl->iq);
     if (lead) {
       const int iq = ctl->iq;
-      update_r_lead(iq);
       int l = 0;
       double t1 = inf;
       for (int k = p; k < iq; k++)
@@ -685,9 +774,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
           t1 = uv[k] / rv[k];
           l = Av[k];
         }
-      double t2;
-      const double zz = dot_lead(zv, zv);
-      const double znp = dot_lead(zv, npv);
+      double t2, zz, znp;
+      dot2_lead(zz, znp);
       if (fabs(zz) > kEps) {
         t2 = -sv[ctl->ip] / znp;
         if (t2 < 0) t2 = inf;  // Takano Akio patch
