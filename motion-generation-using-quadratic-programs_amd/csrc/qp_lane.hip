@@ -56,6 +56,12 @@ struct RIdx {
 };
 
 constexpr int kStage = 5120;  // staging buffer, doubles (40 KiB: 4 waves per CU)
+// rows of the l1 scan in flight per lane (software pipeline depth; CI rows + the ci0 row)
+#ifndef QPGPU_SCAN_DEPTH
+#define QPGPU_SCAN_DEPTH 2
+#endif
+constexpr int kScanDepth = QPGPU_SCAN_DEPTH;
+static_assert(kScanDepth >= 2, "the pipelined scan needs at least two row buffers");
 
 __device__ __forceinline__ bool wave_any(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
 
@@ -606,7 +612,6 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
         // scheduler) before row j is consumed, so one memory latency covers two rows instead
         // of the scheduler's one-load-at-a-time minimum-pressure order.
         if (do_scan) {
-          double rowbuf[2][MM];
           // QP-major rows of an EXACT even-m shape are 16-B aligned when the arrays are
           // (checked on the host: kArgAligned16): load them as dwordx4, half the instructions
           // and half the cache-line lookups per row
@@ -625,47 +630,45 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
               for (int i = 0; i < MM; i++) dst[i] = (i < m) ? src[i] : 0.0;
             }
           };
-          if constexpr (T == 1)
-            ldrow(rowbuf[0], CIg);
-          else
+          // "rows" 0..NM-1 are CI's rows (those >= n are never read), row NM is ci0; row r lands
+          // in rowbuf[r % D], issued D-1 rows ahead of its use
+          constexpr int D = kScanDepth;
+          double rowbuf[D][MM];
+          auto load_row = [&](int r, double* dst) {
+            if (r < NM) {
+              if (r < n) {
+                if constexpr (T == 1)
+                  ldrow(dst, CIg + r * m);
+                else
 #pragma unroll
-            for (int i = 0; i < MM; i++) rowbuf[0][i] = (i < m) ? ldCI(i) : 0.0;
-#pragma unroll
-          for (int j = 0; j < NM; j++) {
-            if (j + 1 < NM) {
-              if constexpr (T == 1) {
-                if (j + 1 < n) ldrow(rowbuf[(j + 1) & 1], CIg + (j + 1) * m);
-              } else {
-#pragma unroll
-                for (int i = 0; i < MM; i++)
-                  rowbuf[(j + 1) & 1][i] = (j + 1 < n && i < m) ? ldCI((j + 1) * m + i) : 0.0;
+                  for (int i = 0; i < MM; i++) dst[i] = (i < m) ? ldCI(r * m + i) : 0.0;
               }
-            } else {
+            } else if (r == NM) {
               if constexpr (T == 1)
-                ldrow(rowbuf[(j + 1) & 1], ci0g);
+                ldrow(dst, ci0g);
               else
 #pragma unroll
-                for (int i = 0; i < MM; i++) rowbuf[(j + 1) & 1][i] = (i < m) ? ldci0(i) : 0.0;
+                for (int i = 0; i < MM; i++) dst[i] = (i < m) ? ldci0(i) : 0.0;
             }
+          };
+#pragma unroll
+          for (int r = 0; r < D - 1; r++) load_row(r, rowbuf[r % D]);
+#pragma unroll
+          for (int j = 0; j < NM; j++) {
+            load_row(j + D - 1, rowbuf[(j + D - 1) % D]);
             __builtin_amdgcn_sched_barrier(0);
             if (j < n) {
               const double xj = xv[j];
 #pragma unroll
               for (int i = 0; i < MM; i++)
-                if (i < m) sv[i] += rowbuf[j & 1][i] * xj;
+                if (i < m) sv[i] += rowbuf[j % D][i] * xj;
             }
             __builtin_amdgcn_sched_barrier(0);
-          }
-          if constexpr (!EXACT) {
-            if (n < NM) {  // ci0 was not fetched by the pipelined tail
-#pragma unroll
-              for (int i = 0; i < MM; i++) rowbuf[NM & 1][i] = (i < m) ? ldci0(i) : 0.0;
-            }
           }
 #pragma unroll
           for (int i = 0; i < MM; i++)
             if (i < m) {
-              sv[i] += rowbuf[NM & 1][i];
+              sv[i] += rowbuf[NM % D][i];
               psi += (sv[i] < 0.0) ? sv[i] : 0.0;
             }
         }
