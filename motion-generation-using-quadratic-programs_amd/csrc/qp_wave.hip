@@ -106,36 +106,41 @@ template <int S, int NMAX, int MMAX, bool GJR>
 struct WaveCfg {
   static constexpr int QPB = S >= 64 ? 1 : 64 / S;  // QPs per block
   static constexpr int BS = S >= 64 ? S : 64;       // threads per block
-  static constexpr int JS = NMAX + 1;               // row stride of J and R
-  // LDS doubles per QP
-  static constexpr int OFF_J = 0;
-  static constexpr int OFF_R = GJR ? 0 : OFF_J + NMAX * JS;
-  static constexpr int OFF_V = GJR ? 0 : OFF_R + NMAX * JS;
-  static constexpr int OFF_X = OFF_V, OFF_Z = OFF_X + NMAX, OFF_D = OFF_Z + NMAX, OFF_NP = OFF_D + NMAX;
-  static constexpr int OFF_RR = OFF_NP + NMAX, OFF_XO = OFF_RR + NMAX;
-  static constexpr int OFF_GC = OFF_XO + NMAX, OFF_GS = OFF_GC + NMAX, OFF_GX = OFF_GS + NMAX;
-  static constexpr int OFF_GF = OFF_GX + NMAX;  // Givens step applied (1.0) / skipped (0.0)
-  static constexpr int OFF_U = OFF_GF + NMAX, OFF_UO = OFF_U + NMAX + 1;
-  static constexpr int OFF_S = OFF_UO + NMAX + 1;
-  static constexpr int OFF_A = OFF_S + MMAX;                        // int[NMAX+1] x 2
-  static constexpr int OFF_FL = OFF_A + (2 * (NMAX + 1) + 1) / 2;  // uint8[MMAX] x 2
-  static constexpr int OFF_CTL = OFF_FL + (2 * MMAX + 7) / 8;
-  static constexpr int PER_QP = OFF_CTL + (int)(sizeof(Ctl) / 8);
-  static constexpr int STRIDE = PER_QP | 1;
-  static constexpr int LDS_DOUBLES = QPB * STRIDE;
-  static_assert(!GJR || JS == BigWs<NMAX>::JS, "workspace layout shared with qp_panel.hip");
   static constexpr int64_t WS_DOUBLES = GJR ? BigWs<NMAX>::PER_QP : 0;  // per QP, global workspace
 };
+
+// LDS layout of one QP, sized by the launch's (n, m) rather than the size class's (NMAX, MMAX),
+// so a problem below the class bound takes only what it needs (C3, n = 30 in the n <= 32
+// class: 37 KiB per two-QP block instead of 42 KiB, i.e. 4 blocks per CU instead of 3, one
+// wave on every SIMD).  J and R are [n][js] with an odd row stride js, so walks down a column
+// (lane = row) are LDS-bank-conflict free; with GJR they live in the workspace instead.
+// Vectors: x z d np r x_old gc gs gx gf (n each), u u_old (n+1 each), s (m), then int A A_old
+// (n+1 each), uint8 act exc (m each) and the control block.
+struct WaveLay {
+  int js, off_r, off_x, off_a, off_fl, off_ctl, stride;
+};
+__host__ __device__ inline WaveLay wave_lay(int n, int m, bool gjr) {
+  WaveLay L;
+  L.js = (n + 1) | 1;
+  L.off_r = gjr ? 0 : n * L.js;
+  L.off_x = gjr ? 0 : 2 * n * L.js;
+  L.off_a = L.off_x + 10 * n + 2 * (n + 1) + m;
+  L.off_fl = L.off_a + (2 * (n + 1) + 1) / 2;
+  L.off_ctl = L.off_fl + (2 * m + 7) / 8;
+  L.stride = (L.off_ctl + (int)((sizeof(Ctl) + 7) / 8)) | 1;
+  return L;
+}
 
 template <int S, int NMAX, int MMAX, bool GJR>
 __global__ void __launch_bounds__(S >= 64 ? S : 64)
     qp_wave_kernel(const QpArgs a, double* __restrict__ ws) {
   using C = WaveCfg<S, NMAX, MMAX, GJR>;
-  constexpr int JS = C::JS;
   // loads in flight per lane in the global-operand sums (deeper for the one-QP-per-workgroup
   // workspace variant, whose lanes have registers to spare)
   constexpr int KG = GJR ? 16 : kUG;
-  __shared__ double lds[C::LDS_DOUBLES];
+  extern __shared__ double lds[];
+  const WaveLay Ly = wave_lay(a.n, a.m, GJR);
+  const int JS = GJR ? BigWs<NMAX>::JS : Ly.js;
 
   const int tid = threadIdx.x;
   const int sg = S >= 64 ? 0 : tid / S;
@@ -144,27 +149,28 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64)
   const int64_t b = (int64_t)blockIdx.x * C::QPB + sg;
   const bool live = b < a.batch;  // whole subgroups only
 
-  double* const Q = lds + sg * C::STRIDE;
-  double* const Jm = GJR ? ws + (b < a.batch ? b : 0) * (int64_t)C::WS_DOUBLES : Q + C::OFF_J;
-  double* const Rm = GJR ? Jm + NMAX * JS : Q + C::OFF_R;
-  double* const xv = Q + C::OFF_X;
-  double* const zv = Q + C::OFF_Z;
-  double* const dv = Q + C::OFF_D;
-  double* const npv = Q + C::OFF_NP;
-  double* const rv = Q + C::OFF_RR;
-  double* const xo = Q + C::OFF_XO;
-  double* const gc = Q + C::OFF_GC;
-  double* const gs = Q + C::OFF_GS;
-  double* const gx = Q + C::OFF_GX;
-  double* const gf = Q + C::OFF_GF;
-  double* const uv = Q + C::OFF_U;
-  double* const uo = Q + C::OFF_UO;
-  double* const sv = Q + C::OFF_S;
-  int* const Av = reinterpret_cast<int*>(Q + C::OFF_A);
-  int* const Ao = Av + NMAX + 1;
-  uint8_t* const act = reinterpret_cast<uint8_t*>(Q + C::OFF_FL);  // iai[i] == -1
-  uint8_t* const exc = act + MMAX;                                  // !iaexcl[i]
-  Ctl* const ctl = reinterpret_cast<Ctl*>(Q + C::OFF_CTL);
+  double* const Q = lds + sg * Ly.stride;
+  double* const Jm = GJR ? ws + (b < a.batch ? b : 0) * (int64_t)C::WS_DOUBLES : Q;
+  double* const Rm = GJR ? Jm + BigWs<NMAX>::OFF_R : Q + Ly.off_r;
+  const int nv = a.n;
+  double* const xv = Q + Ly.off_x;
+  double* const zv = xv + nv;
+  double* const dv = zv + nv;
+  double* const npv = dv + nv;
+  double* const rv = npv + nv;
+  double* const xo = rv + nv;
+  double* const gc = xo + nv;
+  double* const gs = gc + nv;
+  double* const gx = gs + nv;
+  double* const gf = gx + nv;  // Givens step applied (1.0) / skipped (0.0)
+  double* const uv = gf + nv;
+  double* const uo = uv + nv + 1;
+  double* const sv = uo + nv + 1;
+  int* const Av = reinterpret_cast<int*>(Q + Ly.off_a);
+  int* const Ao = Av + nv + 1;
+  uint8_t* const act = reinterpret_cast<uint8_t*>(Q + Ly.off_fl);  // iai[i] == -1
+  uint8_t* const exc = act + a.m;                                   // !iaexcl[i]
+  Ctl* const ctl = reinterpret_cast<Ctl*>(Q + Ly.off_ctl);
 
   const int n = a.n, p = a.p, m = a.m, T = a.tile;
   const double inf = dinf();
@@ -893,7 +899,16 @@ template <int S, int NMAX, int MMAX, bool GJR>
 static hipError_t launch_wave(const QpArgs& a, hipStream_t stream, double* ws) {
   using C = WaveCfg<S, NMAX, MMAX, GJR>;
   const int64_t blocks = (a.batch + C::QPB - 1) / C::QPB;
-  hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR>), dim3((unsigned)blocks), dim3(C::BS), 0,
+  const size_t lds_bytes = (size_t)C::QPB * wave_lay(a.n, a.m, GJR).stride * sizeof(double);
+  static size_t granted = 0;  // dynamic LDS beyond 64 KiB must be granted per kernel
+  if (lds_bytes > 65536 && lds_bytes > granted) {
+    const hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&qp_wave_kernel<S, NMAX, MMAX, GJR>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    if (e != hipSuccess) return e;
+    granted = lds_bytes;
+  }
+  hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR>), dim3((unsigned)blocks), dim3(C::BS), lds_bytes,
                      stream, a, ws);
   return hipGetLastError();
 }
