@@ -125,11 +125,18 @@ int qpgpu_max_m(void) {
   return mm > 64 ? mm : 64;
 }
 
+// Default family order: lane (n <= 8, m <= 16), then the subgroup kernel only where it is the
+// faster one — n <= 8, m <= 32 (its S = 8 variants) — then the wave kernels.  Measured on MI355X
+// with 65 536 QPs per launch (profiles/r01_s2/family_crossover.log): the wave family's
+// runtime-sized LDS layout beats the S = 16 subgroup kernel from n = 9 up (n = 14, m = 28:
+// 2.2 vs 3.5 ms) and at m = 64; the S = 8 subgroup kernel still wins at n <= 8, m <= 32.
+static bool default_small(int n, int m) { return n <= 8 && m <= 32; }
+
 const char* qpgpu_kernel_name(int32_t n, int32_t p, int32_t m) {
   if (n <= 0 || p < 0 || m < 0) return "";
   const char* s = qpk_lane_name(n, p, m);
   if (s) return s;
-  s = qpk_small_name(n, p, m);
+  s = default_small(n, m) ? qpk_small_name(n, p, m) : nullptr;
   if (s) return s;
   s = qpk_medium_name(n, p, m);
   return s ? s : "";
@@ -214,7 +221,7 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
     wrc = launch_wave();
   } else {
     e = qpk_launch_lane(&a, s, &handled, nullptr);
-    if (!handled) e = qpk_launch_small(&a, s, &handled, nullptr);
+    if (!handled && default_small(a.n, a.m)) e = qpk_launch_small(&a, s, &handled, nullptr);
     if (!handled) wrc = launch_wave();
   }
   if (wrc) return wrc;
