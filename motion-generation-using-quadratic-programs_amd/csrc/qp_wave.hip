@@ -31,19 +31,38 @@ __device__ __forceinline__ void grp_sync() {
 // (or LDS) operands costs one memory latency per chunk instead of one per element.  The adds
 // stay strictly sequential in the reference's index order, so results are bit-identical.
 // Chunk sizes: operands in global memory (CI always; J and R with GJR) batch kUG loads per
-// chunk; LDS-resident operands use plain sequential loops (kUL = 1).
-constexpr int kUG = 8, kUL = 1;
+// chunk; LDS-resident operands batch kUL.
+#ifndef QPGPU_WAVE_KUL
+#define QPGPU_WAVE_KUL 4
+#endif
+constexpr int kUG = 8, kUL = QPGPU_WAVE_KUL;
 
-// s + sum_{j=j0}^{j1-1} A(j) * B(j), j ascending (s += a*b per element)
+// s + sum_{j=j0}^{j1-1} A(j) * B(j), j ascending (s += a*b per element).  Full chunks of kU
+// issue all their loads unpredicated before the chunk's multiply-adds; the remainder is one
+// predicated chunk.
 template <int kU, class FA, class FB>
 __device__ __forceinline__ double seq_fma_up(double s, int j0, int j1, FA A, FB B) {
-  for (int jb = j0; jb < j1; jb += kU) {
+  if constexpr (kU == 1) {
+    for (int j = j0; j < j1; j++) s += A(j) * B(j);
+    return s;
+  }
+  int jb = j0;
+  for (; jb + kU <= j1; jb += kU) {
     double va[kU], vb[kU];
 #pragma unroll
     for (int u = 0; u < kU; u++) {
-      const int j = jb + u;
-      va[u] = j < j1 ? A(j) : 0.0;
-      vb[u] = j < j1 ? B(j) : 0.0;
+      va[u] = A(jb + u);
+      vb[u] = B(jb + u);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) s += va[u] * vb[u];
+  }
+  if (jb < j1) {  // partial chunk: loads predicated, still one latency
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      va[u] = jb + u < j1 ? A(jb + u) : 0.0;
+      vb[u] = jb + u < j1 ? B(jb + u) : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < kU; u++)
@@ -55,13 +74,27 @@ __device__ __forceinline__ double seq_fma_up(double s, int j0, int j1, FA A, FB 
 // s - sum A(j) * B(j), j ascending (s -= a*b per element)
 template <int kU, class FA, class FB>
 __device__ __forceinline__ double seq_fms_up(double s, int j0, int j1, FA A, FB B) {
-  for (int jb = j0; jb < j1; jb += kU) {
+  if constexpr (kU == 1) {
+    for (int j = j0; j < j1; j++) s -= A(j) * B(j);
+    return s;
+  }
+  int jb = j0;
+  for (; jb + kU <= j1; jb += kU) {
     double va[kU], vb[kU];
 #pragma unroll
     for (int u = 0; u < kU; u++) {
-      const int j = jb + u;
-      va[u] = j < j1 ? A(j) : 0.0;
-      vb[u] = j < j1 ? B(j) : 0.0;
+      va[u] = A(jb + u);
+      vb[u] = B(jb + u);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) s -= va[u] * vb[u];
+  }
+  if (jb < j1) {
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      va[u] = jb + u < j1 ? A(jb + u) : 0.0;
+      vb[u] = jb + u < j1 ? B(jb + u) : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < kU; u++)
@@ -73,13 +106,27 @@ __device__ __forceinline__ double seq_fms_up(double s, int j0, int j1, FA A, FB 
 // s - sum A(k) * B(k), k DEscending from k1-1 down to k0 (s -= a*b per element)
 template <int kU, class FA, class FB>
 __device__ __forceinline__ double seq_fms_down(double s, int k0, int k1, FA A, FB B) {
-  for (int kb = k1 - 1; kb >= k0; kb -= kU) {
+  if constexpr (kU == 1) {
+    for (int k = k1 - 1; k >= k0; k--) s -= A(k) * B(k);
+    return s;
+  }
+  int kb = k1 - 1;
+  for (; kb - kU + 1 >= k0; kb -= kU) {
     double va[kU], vb[kU];
 #pragma unroll
     for (int u = 0; u < kU; u++) {
-      const int k = kb - u;
-      va[u] = k >= k0 ? A(k) : 0.0;
-      vb[u] = k >= k0 ? B(k) : 0.0;
+      va[u] = A(kb - u);
+      vb[u] = B(kb - u);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) s -= va[u] * vb[u];
+  }
+  if (kb >= k0) {
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      va[u] = kb - u >= k0 ? A(kb - u) : 0.0;
+      vb[u] = kb - u >= k0 ? B(kb - u) : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < kU; u++)
