@@ -61,6 +61,14 @@ constexpr int kStage = 5120;  // staging buffer, doubles (40 KiB: 4 waves per CU
 #define QPGPU_SCAN_DEPTH 2
 #endif
 constexpr int kScanDepth = QPGPU_SCAN_DEPTH;
+// warm the caches with this lane's CI / ci0 lines before the equality phase (QP-major layout).
+// Off by default: measured (profiles/r01_s2/lane_ci_warmup.log) it shortens the mean wave (scan
+// 36k -> 28k cycles) but lowers the pipelined throughput ~4 % on C1 and C2 — the extra
+// uncoalesced loads compete with other launches' scans.
+#ifndef QPGPU_LANE_PREFETCH
+#define QPGPU_LANE_PREFETCH 0
+#endif
+constexpr bool kLanePrefetch = QPGPU_LANE_PREFETCH != 0;
 static_assert(kScanDepth >= 2, "the pipelined scan needs at least two row buffers");
 
 __device__ __forceinline__ bool wave_any(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
@@ -144,6 +152,9 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   static_assert(RB_A + QPW * (NM + 1) <= STAGE, "LDS regions exceed the stage buffer");
 #define Jr_(i, j) sbuf[((i) * NM + (j)) * QPW + lane]
   double CEr[NM][NM], ce0r[NM];  // CEr[i][j] = CE[j][i] (column i = equality constraint i)
+  // one dword per 128-B line of this lane's CI / ci0 blocks (cache warm-up, see below)
+  constexpr int kPfCI = (NM * MM * 8 + 127) / 128 + 1, kPfC0 = (MM * 8 + 127) / 128 + 1;
+  [[maybe_unused]] uint32_t pf[kPfCI + kPfC0];
   qp_stamp(a, 0);
 
   // ---------------------------------------------------------------- setup
@@ -299,6 +310,23 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
     }
   }
   qp_stamp(a, 1);
+  // Touch every cache line of this lane's CI and ci0 blocks before the equality phase: the
+  // loads complete during it (nothing waits on them until its end), so the first l1 scan — all
+  // lanes of every wave at about the same time — reads L2 / MALL instead of queueing on one
+  // chip-wide HBM burst.
+  if constexpr (T == 1 && kLanePrefetch) {
+    if (live) {
+      const char* c = reinterpret_cast<const char*>(a.CI + b * (int64_t)(n * m));
+      const char* c0 = reinterpret_cast<const char*>(a.ci0 + b * (int64_t)m);
+      const int bc = n * m * 8, b0c = m * 8;
+#pragma unroll
+      for (int k = 0; k < kPfCI; k++)
+        pf[k] = (bc >= 4) ? *reinterpret_cast<const uint32_t*>(c + min(k * 128, bc - 4)) : 0u;
+#pragma unroll
+      for (int k = 0; k < kPfC0; k++)
+        pf[kPfCI + k] = (b0c >= 4) ? *reinterpret_cast<const uint32_t*>(c0 + min(k * 128, b0c - 4)) : 0u;
+    }
+  }
   if (!chol_ok) {
     status = QPGPU_QP_NOT_POSITIVE_DEFINITE;
     fval = bad_sum;
@@ -538,6 +566,11 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
     }
     a.f_eq[b] = fval;
     a.st_eq[b] = status;
+  }
+  if constexpr (T == 1 && kLanePrefetch) {
+    if (live)  // the warm-up loads retire here, long after they landed
+#pragma unroll
+      for (int k = 0; k < kPfCI + kPfC0; k++) asm volatile("" ::"v"(pf[k]));
   }
   qp_stamp(a, 2);
 
