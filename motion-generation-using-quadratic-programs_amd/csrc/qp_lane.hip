@@ -19,6 +19,7 @@
 // IEEE binary64 throughout, no contraction: results are bitwise identical to the CPU
 // restatement (oracle/qp_oracle.c), which tests/ check.
 #include <cstdlib>
+#include <type_traits>
 
 #include "qp_common.h"
 
@@ -30,18 +31,27 @@ __device__ __forceinline__ T opq_l(T v) {
   return v;
 }
 
-template <int N, typename T>
-__device__ __forceinline__ T lsel(const T (&v)[N], int i) {
-  T r = opq_l(v[0]);
+// v[i] / v[i] = x for a run-time i known to be >= LO (entries below LO are never selected)
+template <int LO, int N, typename T>
+__device__ __forceinline__ T lsel_lo(const T (&v)[N], int i) {
+  T r = opq_l(v[LO]);
 #pragma unroll
-  for (int k = 1; k < N; k++) r = (k == i) ? opq_l(v[k]) : r;
+  for (int k = LO + 1; k < N; k++) r = (k == i) ? opq_l(v[k]) : r;
   return r;
 }
+template <int N, typename T>
+__device__ __forceinline__ T lsel(const T (&v)[N], int i) {
+  return lsel_lo<0>(v, i);
+}
 
+template <int LO, int N, typename T>
+__device__ __forceinline__ void lput_lo(T (&v)[N], int i, T x) {
+#pragma unroll
+  for (int k = LO; k < N; k++) v[k] = (k == i) ? x : v[k];
+}
 template <int N, typename T>
 __device__ __forceinline__ void lput(T (&v)[N], int i, T x) {
-#pragma unroll
-  for (int k = 0; k < N; k++) v[k] = (k == i) ? x : v[k];
+  lput_lo<0>(v, i, x);
 }
 
 // R storage: packed upper triangle (row-major) followed by the first subdiagonal.
@@ -381,10 +391,15 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
       }
     }
   };
-  auto add_constraint = [&]() -> bool {
+  // LoC: a compile-time lower bound on iq (std::integral_constant).  In the active-set loop
+  // iq >= p always (equality constraints are never dropped), so entries below p of R, A, u and
+  // d are never the ones written or selected there: with p a compile-time constant (PX) the
+  // predicated updates of those entries disappear.
+  auto add_constraint = [&](auto LoC) -> bool {
+    constexpr int LO = decltype(LoC)::value;
     if (iq >= n) return false;  // reference UB (p > n); reported as dependent
 #pragma unroll
-    for (int j = NM - 1; j >= 1; j--) {
+    for (int j = NM - 1; j >= LO + 1; j--) {
       if (j <= n - 1 && j >= iq + 1) {
         double cc = dv[j - 1], ss = dv[j];
         const double h = qp_distance(cc, ss);
@@ -414,18 +429,19 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
     iq++;
     // R[:iq, iq-1] = d[:iq]
 #pragma unroll
-    for (int c = 0; c < NM; c++)
+    for (int c = LO; c < NM; c++)
 #pragma unroll
       for (int i = 0; i <= c; i++) {
         const bool w = (c == iq - 1);
         Rv[RI::at(i, c)] = w ? dv[i] : Rv[RI::at(i, c)];
       }
-    const double dd = fabs(lsel<NM>(dv, iq - 1));
+    const double dd = fabs(lsel_lo<LO < NM ? LO : NM - 1>(dv, iq - 1));
     if (dd <= kEps * R_norm) return false;
     R_norm = (R_norm < dd) ? dd : R_norm;
     return true;
   };
-  auto delete_constraint = [&](int l) {
+  auto delete_constraint = [&](int l, auto LoC) {
+    constexpr int LO = decltype(LoC)::value;  // qq >= LO (the deleted constraint is an inequality)
     int qq = 0;
     bool found = false;
 #pragma unroll
@@ -435,14 +451,14 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
         found = true;
       }
 #pragma unroll
-    for (int i = 0; i < NM; i++)
+    for (int i = LO; i < NM; i++)
       if (i >= qq && i < iq - 1) {
         Av[i] = Av[i + 1];
         uv[i] = uv[i + 1];
       }
     // shift R columns left from qq (only upper + subdiagonal entries exist)
 #pragma unroll
-    for (int c = 0; c < NM - 1; c++) {
+    for (int c = LO; c < NM - 1; c++) {
       const bool sh = (c >= qq && c < iq - 1);
 #pragma unroll
       for (int r = 0; r <= c + 1 && r < NM; r++) {
@@ -451,16 +467,16 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
       }
     }
     {
-      const int aiq = lsel<NM + 1>(Av, iq);
-      const double uiq = lsel<NM + 1>(uv, iq);
-      lput<NM + 1>(Av, iq - 1, aiq);
-      lput<NM + 1>(uv, iq - 1, uiq);
-      lput<NM + 1>(Av, iq, 0);
-      lput<NM + 1>(uv, iq, 0.0);
+      const int aiq = lsel_lo<LO>(Av, iq);
+      const double uiq = lsel_lo<LO>(uv, iq);
+      lput_lo<LO>(Av, iq - 1, aiq);
+      lput_lo<LO>(uv, iq - 1, uiq);
+      lput_lo<LO>(Av, iq, 0);
+      lput_lo<LO>(uv, iq, 0.0);
     }
     // R[j][iq-1] = 0 for j < iq
 #pragma unroll
-    for (int c = 0; c < NM; c++)
+    for (int c = LO; c < NM; c++)
 #pragma unroll
       for (int r = 0; r <= c + 1 && r < NM; r++) {
         const bool z = (c == iq - 1) && (r < iq);
@@ -469,7 +485,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
     iq--;
     if (iq == 0) return;
 #pragma unroll
-    for (int j = 0; j < NM - 1; j++) {
+    for (int j = LO; j < NM - 1; j++) {
       if (j >= qq && j < iq) {
         double cc = Rv[RI::at(j, j)], ss = Rv[RI::at(j + 1, j)];
         const double h = qp_distance(cc, ss);
@@ -548,7 +564,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
         if (k < i) uv[k] -= t2 * rv[k];
       fval += 0.5 * (t2 * t2) * znp;
       Av[i < NM + 1 ? i : NM] = -i - 1;
-      if (!add_constraint()) {
+      if (!add_constraint(std::integral_constant<int, 0>{})) {
         status = QPGPU_QP_DEPENDENT;
         done = true;
       }
@@ -577,6 +593,10 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   // ---------------------------------------------------------------- active-set loop
   // Wave-uniform loop: every lane stays until all 64 are done, so the cooperative CI staging
   // and its barriers are reached by the whole wave; per-lane work is predicated on `active`.
+  // Every active lane has iq >= p here (the equality phase completed, only inequalities are
+  // ever dropped), so with p known at compile time the loop's iq-indexed updates start at p.
+  constexpr int IQLO = PX >= 0 ? (PX <= NM ? PX : NM) : 0;
+  const auto kLo = std::integral_constant<int, IQLO>{};
   {
     double sv[MM];
 #pragma unroll
@@ -740,8 +760,8 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
 #pragma unroll
           for (int j = 0; j < NM; j++) npv[j] = (j < n) ? ldCI(j * m + ip) : 0.0;
           ci0ip = ldci0(ip);
-          lput<NM + 1>(uv, iq, 0.0);
-          lput<NM + 1>(Av, iq, ip);
+          lput_lo<IQLO>(uv, iq, 0.0);
+          lput_lo<IQLO>(Av, iq, ip);
         }
       }
       if (a.stamps) {
@@ -789,22 +809,22 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
 #pragma unroll
             for (int k = 0; k < NM; k++)
               if (k < iq) uv[k] -= t * rv[k];
-            lput<NM + 1>(uv, iq, lsel<NM + 1>(uv, iq) + t);
+            lput_lo<IQLO>(uv, iq, lsel_lo<IQLO>(uv, iq) + t);
             act &= ~(1ull << l);
-            delete_constraint(l);
+            delete_constraint(l, kLo);
             need_scan = need_select = false;
           } else {
 #pragma unroll
             for (int k = 0; k < NM; k++) xv[k] += t * zv[k];
-            fval += t * znp * (0.5 * t + lsel<NM + 1>(uv, iq));
+            fval += t * znp * (0.5 * t + lsel_lo<IQLO>(uv, iq));
 #pragma unroll
             for (int k = 0; k < NM; k++)
               if (k < iq) uv[k] -= t * rv[k];
-            lput<NM + 1>(uv, iq, lsel<NM + 1>(uv, iq) + t);
+            lput_lo<IQLO>(uv, iq, lsel_lo<IQLO>(uv, iq) + t);
             if (fabs(t - t2) < kEps) {  // full step
-              if (!add_constraint()) {
+              if (!add_constraint(kLo)) {
                 excl |= 1ull << ip;
-                delete_constraint(ip);
+                delete_constraint(ip, kLo);
                 act = 0;
 #pragma unroll
                 for (int i = 0; i < NM; i++)
@@ -823,7 +843,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
               }
             } else {  // partial step: drop l, refresh s[ip] = CI[:,ip]^T x + ci0[ip]
               act &= ~(1ull << l);
-              delete_constraint(l);
+              delete_constraint(l, kLo);
               double s = 0.0;
 #pragma unroll
               for (int j = 0; j < NM; j++)
