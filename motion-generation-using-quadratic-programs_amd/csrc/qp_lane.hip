@@ -161,7 +161,11 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   constexpr int RB_U = RB + QPW * NM, RB_A = RB_U + QPW * (NM + 1);
   static_assert(RB_A + QPW * (NM + 1) <= STAGE, "LDS regions exceed the stage buffer");
 #define Jr_(i, j) sbuf[((i) * NM + (j)) * QPW + lane]
-  double CEr[NM][NM], ce0r[NM];  // CEr[i][j] = CE[j][i] (column i = equality constraint i)
+  // J lives in registers (compile-time indices) through the J build and the equality phase,
+  // where every step reads and rotates all of it; the loop then works on its LDS image.  CE
+  // and ce0 stay in their LDS staging (read once per equality step) until then.
+  double Jreg[NM][NM];
+  bool ce_staged = false;
   // one dword per 128-B line of this lane's CI / ci0 blocks (cache warm-up, see below)
   constexpr int kPfCI = (NM * MM * 8 + 127) / 128 + 1, kPfC0 = (MM * 8 + 127) / 128 + 1;
   [[maybe_unused]] uint32_t pf[kPfCI + kPfC0];
@@ -235,22 +239,8 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
     if (p > 0) {
       const int np_ = n * p;
       const int offc = (QPW * np_ + 127) / 128 * 128;
-      const bool staged = offc + QPW * p <= STAGE;
-      __syncthreads();
-  #pragma unroll
-      for (int i = 0; i < NM; i++) {
-  #pragma unroll
-        for (int j = 0; j < NM; j++) {
-          double v = 0.0;
-          if (live && i < p && j < n)
-            v = staged ? rd_all(0, np_, j * p + i) : view(const_cast<double*>(a.CE), np_)[(j * p + i) * T];
-          CEr[i][j] = v;
-        }
-        double c0 = 0.0;
-        if (live && i < p) c0 = staged ? rd_all(offc, p, i) : view(const_cast<double*>(a.ce0), p)[i * T];
-        ce0r[i] = c0;
-      }
-      __syncthreads();
+      ce_staged = offc + QPW * p <= STAGE;
+      __syncthreads();  // the staged CE / ce0 are read in the equality phase
     }
     if (chol_ok) {
       // J = L^{-T}: row r of J = L^{-1} e_r (forward_elimination); c2 = trace(J).
@@ -280,7 +270,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
             y[i] = v;
           }
 #pragma unroll
-          for (int j = 0; j < NM; j++) Jr_(r, j) = y[j];
+          for (int j = 0; j < NM; j++) Jreg[r][j] = y[j];
           if (r < n) c2 += y[r];
         }
       };
@@ -359,34 +349,46 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   double R_norm = 1.0;
   int iq = 0;
 
-    auto compute_d = [&]() {
+  // InReg: std::true_type = J in Jreg (setup / equality phase), false_type = LDS image (loop)
+  auto Jat = [&](auto InReg, int i, int j) -> double& {
+    if constexpr (decltype(InReg)::value)
+      return Jreg[i][j];
+    else
+      return Jr_(i, j);
+  };
+  const auto kReg = std::true_type{};
+  const auto kLds = std::false_type{};
+  auto compute_d = [&](auto InReg) {
 #pragma unroll
     for (int c = 0; c < NM; c++) {
       double s = 0.0;
 #pragma unroll
       for (int j = 0; j < NM; j++)
-        if (j < n) s += Jr_(j, c) * npv[j];
+        if (j < n) s += Jat(InReg, j, c) * npv[j];
       dv[c] = s;
     }
   };
-  auto update_z = [&]() {
+  // LoC: compile-time lower bound on iq (see add_constraint below)
+  auto update_z = [&](auto InReg, auto LoC) {
+    constexpr int LO = decltype(LoC)::value;
 #pragma unroll
     for (int r = 0; r < NM; r++) {
       double z = 0.0;
 #pragma unroll
-      for (int j = 0; j < NM; j++)
-        if (j >= iq && j < n) z += Jr_(r, j) * dv[j];
+      for (int j = LO; j < NM; j++)
+        if (j >= iq && j < n) z += Jat(InReg, r, j) * dv[j];
       zv[r] = z;
     }
   };
-  auto update_r = [&]() {
+  auto update_r = [&](auto LoC) {
+    constexpr int LO = decltype(LoC)::value;
 #pragma unroll
     for (int i = NM - 1; i >= 0; i--) {
-      if (i < iq) {
+      if (i < LO || i < iq) {
         double s = 0.0;
 #pragma unroll
         for (int j = i + 1; j < NM; j++)
-          if (j < iq) s += Rv[RI::at(i, j)] * rv[j];
+          if (j < LO || j < iq) s += Rv[RI::at(i, j)] * rv[j];
         rv[i] = (dv[i] - s) / Rv[RI::at(i, i)];
       }
     }
@@ -395,7 +397,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   // iq >= p always (equality constraints are never dropped), so entries below p of R, A, u and
   // d are never the ones written or selected there: with p a compile-time constant (PX) the
   // predicated updates of those entries disappear.
-  auto add_constraint = [&](auto LoC) -> bool {
+  auto add_constraint = [&](auto InReg, auto LoC) -> bool {
     constexpr int LO = decltype(LoC)::value;
     if (iq >= n) return false;  // reference UB (p > n); reported as dependent
 #pragma unroll
@@ -418,10 +420,10 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
 #pragma unroll
           for (int k = 0; k < NM; k++)
             if (k < n) {
-              const double t1 = Jr_(k, j - 1), t2 = Jr_(k, j);
+              const double t1 = Jat(InReg, k, j - 1), t2 = Jat(InReg, k, j);
               const double n1 = t1 * cc + t2 * ss;
-              Jr_(k, j - 1) = n1;
-              Jr_(k, j) = xny * (t1 + n1) - t2;
+              Jat(InReg, k, j - 1) = n1;
+              Jat(InReg, k, j) = xny * (t1 + n1) - t2;
             }
         }
       }
@@ -540,18 +542,23 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
       iq = i;
       double c0;
       if (i < NM) {
+        const int np_ = n * p;
+        const int offc = (QPW * np_ + 127) / 128 * 128;
 #pragma unroll
-        for (int j = 0; j < NM; j++) npv[j] = CEr[i][j];
-        c0 = ce0r[i];
+        for (int j = 0; j < NM; j++)
+          npv[j] = (live && j < n) ? (ce_staged ? rd_all(0, np_, j * p + i)
+                                                : view(const_cast<double*>(a.CE), np_)[(j * p + i) * T])
+                                   : 0.0;
+        c0 = live ? (ce_staged ? rd_all(offc, p, i) : view(const_cast<double*>(a.ce0), p)[i * T]) : 0.0;
       } else {  // p > n: the step that reports "dependent" (reference UB, see oracle)
         const double* CEb = view(const_cast<double*>(a.CE), n * p);
 #pragma unroll
         for (int j = 0; j < NM; j++) npv[j] = (j < n) ? CEb[(j * p + i) * T] : 0.0;
         c0 = view(const_cast<double*>(a.ce0), p)[i * T];
       }
-      compute_d();
-      update_z();
-      update_r();
+      compute_d(kReg);
+      update_z(kReg, std::integral_constant<int, 0>{});
+      update_r(std::integral_constant<int, 0>{});
       double t2 = 0.0;
       const double zz = dot(zv, zv);
       const double znp = dot(zv, npv);
@@ -564,7 +571,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
         if (k < i) uv[k] -= t2 * rv[k];
       fval += 0.5 * (t2 * t2) * znp;
       Av[i < NM + 1 ? i : NM] = -i - 1;
-      if (!add_constraint(std::integral_constant<int, 0>{})) {
+      if (!add_constraint(kReg, std::integral_constant<int, 0>{})) {
         status = QPGPU_QP_DEPENDENT;
         done = true;
       }
@@ -587,6 +594,12 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
     if (live)  // the warm-up loads retire here, long after they landed
 #pragma unroll
       for (int k = 0; k < kPfCI + kPfC0; k++) asm volatile("" ::"v"(pf[k]));
+  }
+  if (ok_lane) {
+#pragma unroll
+    for (int i = 0; i < NM; i++)
+#pragma unroll
+      for (int j = 0; j < NM; j++) Jr_(i, j) = Jreg[i][j];
   }
   qp_stamp(a, 2);
 
@@ -734,7 +747,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
           } else {
 #pragma unroll
             for (int i = 0; i < NM; i++) {
-              if (i < iq) {
+              if (i < IQLO || i < iq) {
                 UOLD(i) = uv[i];
                 AOLD(i) = (double)Av[i];
               }
@@ -778,9 +791,9 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
           status = QPGPU_QP_MAX_ITER;
           active = false;
         } else {
-          compute_d();
-          update_z();
-          update_r();
+          compute_d(kLds);
+          update_z(kLds, kLo);
+          update_r(kLo);
           int l = 0;
           double t1 = inf;
 #pragma unroll
@@ -808,7 +821,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
           } else if (t2 >= inf) {  // dual step only
 #pragma unroll
             for (int k = 0; k < NM; k++)
-              if (k < iq) uv[k] -= t * rv[k];
+              if (k < IQLO || k < iq) uv[k] -= t * rv[k];
             lput_lo<IQLO>(uv, iq, lsel_lo<IQLO>(uv, iq) + t);
             act &= ~(1ull << l);
             delete_constraint(l, kLo);
@@ -819,10 +832,10 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
             fval += t * znp * (0.5 * t + lsel_lo<IQLO>(uv, iq));
 #pragma unroll
             for (int k = 0; k < NM; k++)
-              if (k < iq) uv[k] -= t * rv[k];
+              if (k < IQLO || k < iq) uv[k] -= t * rv[k];
             lput_lo<IQLO>(uv, iq, lsel_lo<IQLO>(uv, iq) + t);
             if (fabs(t - t2) < kEps) {  // full step
-              if (!add_constraint(kLo)) {
+              if (!add_constraint(kLds, kLo)) {
                 excl |= 1ull << ip;
                 delete_constraint(ip, kLo);
                 act = 0;
