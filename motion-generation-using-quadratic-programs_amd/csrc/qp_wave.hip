@@ -178,8 +178,10 @@ __host__ __device__ inline WaveLay wave_lay(int n, int m, bool gjr) {
   return L;
 }
 
-template <int S, int NMAX, int MMAX, bool GJR>
-__global__ void __launch_bounds__(S >= 64 ? S : 64)
+// OCC = minimum waves per SIMD the register allocation must allow (launch-bounds hint): 1, or
+// 4 for the two-QP-per-wave variants when the launch's LDS leaves room for that many (launch_wave)
+template <int S, int NMAX, int MMAX, bool GJR, int OCC = 1>
+__global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
     qp_wave_kernel(const QpArgs a, double* __restrict__ ws) {
   using C = WaveCfg<S, NMAX, MMAX, GJR>;
   // loads in flight per lane in the global-operand sums (deeper for the one-QP-per-workgroup
@@ -947,6 +949,18 @@ static hipError_t launch_wave(const QpArgs& a, hipStream_t stream, double* ws) {
   using C = WaveCfg<S, NMAX, MMAX, GJR>;
   const int64_t blocks = (a.batch + C::QPB - 1) / C::QPB;
   const size_t lds_bytes = (size_t)C::QPB * wave_lay(a.n, a.m, GJR).stride * sizeof(double);
+  // Two-QP-per-wave variants: when a block's LDS leaves room for >= 2 waves per SIMD (<= 20 KiB,
+  // i.e. >= 8 one-wave blocks per CU) register pressure is the occupancy limit, so launch the
+  // instantiation compiled for 4 waves per SIMD (a few spilled VGPRs).  Measured: mgqp level 0
+  // (10.5 KiB per block) 2.44 -> 2.32 ms; C3 (37 KiB per block, LDS-limited to one wave per SIMD)
+  // keeps the unconstrained allocation (21.0 vs 22.0 ms).
+  if constexpr (S < 64 && !GJR) {
+    if (lds_bytes <= 20480) {
+      hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR, 4>), dim3((unsigned)blocks), dim3(C::BS),
+                         lds_bytes, stream, a, ws);
+      return hipGetLastError();
+    }
+  }
   static size_t granted = 0;  // dynamic LDS beyond 64 KiB must be granted per kernel
   if (lds_bytes > 65536 && lds_bytes > granted) {
     const hipError_t e = hipFuncSetAttribute(
