@@ -71,6 +71,9 @@ constexpr int kStage = 5120;  // staging buffer, doubles (40 KiB: 4 waves per CU
 #define QPGPU_SCAN_DEPTH 2
 #endif
 constexpr int kScanDepth = QPGPU_SCAN_DEPTH;
+#ifndef QPGPU_LANE_JREG_LOOP
+#define QPGPU_LANE_JREG_LOOP 2
+#endif
 // warm the caches with this lane's CI / ci0 lines before the equality phase (QP-major layout).
 // Off by default: measured (profiles/r01_s2/lane_ci_warmup.log) it shortens the mean wave (scan
 // 36k -> 28k cycles) but lowers the pipelined throughput ~4 % on C1 and C2 — the extra
@@ -166,6 +169,9 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   // and ce0 stay in their LDS staging (read once per equality step) until then.
   double Jreg[NM][NM];
   bool ce_staged = false;
+  // keep J in registers through the active-set loop too (QPGPU_LANE_JREG_LOOP: 0 never, 1 when
+  // p = 0 — no equality phase, the loop does all the rotations — , 2 always)
+  constexpr bool kJregLoop = QPGPU_LANE_JREG_LOOP == 2 || (QPGPU_LANE_JREG_LOOP == 1 && PX == 0);
   // one dword per 128-B line of this lane's CI / ci0 blocks (cache warm-up, see below)
   constexpr int kPfCI = (NM * MM * 8 + 127) / 128 + 1, kPfC0 = (MM * 8 + 127) / 128 + 1;
   [[maybe_unused]] uint32_t pf[kPfCI + kPfC0];
@@ -442,7 +448,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
     R_norm = (R_norm < dd) ? dd : R_norm;
     return true;
   };
-  auto delete_constraint = [&](int l, auto LoC) {
+  auto delete_constraint = [&](int l, auto InReg, auto LoC) {
     constexpr int LO = decltype(LoC)::value;  // qq >= LO (the deleted constraint is an inequality)
     int qq = 0;
     bool found = false;
@@ -514,10 +520,10 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
 #pragma unroll
           for (int k = 0; k < NM; k++)
             if (k < n) {
-              const double t1 = Jr_(k, j), t2 = Jr_(k, j + 1);
+              const double t1 = Jat(InReg, k, j), t2 = Jat(InReg, k, j + 1);
               const double n1 = t1 * cc + t2 * ss;
-              Jr_(k, j) = n1;
-              Jr_(k, j + 1) = xny * (n1 + t1) - t2;
+              Jat(InReg, k, j) = n1;
+              Jat(InReg, k, j + 1) = xny * (n1 + t1) - t2;
             }
         }
       }
@@ -595,7 +601,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
 #pragma unroll
       for (int k = 0; k < kPfCI + kPfC0; k++) asm volatile("" ::"v"(pf[k]));
   }
-  if (ok_lane) {
+  if (!kJregLoop && ok_lane) {
 #pragma unroll
     for (int i = 0; i < NM; i++)
 #pragma unroll
@@ -610,6 +616,8 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   // ever dropped), so with p known at compile time the loop's iq-indexed updates start at p.
   constexpr int IQLO = PX >= 0 ? (PX <= NM ? PX : NM) : 0;
   const auto kLo = std::integral_constant<int, IQLO>{};
+  // where the loop keeps J: registers (kJregLoop) or the LDS image
+  const auto kJL = std::integral_constant<bool, kJregLoop>{};
   {
     double sv[MM];
 #pragma unroll
@@ -791,8 +799,8 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
           status = QPGPU_QP_MAX_ITER;
           active = false;
         } else {
-          compute_d(kLds);
-          update_z(kLds, kLo);
+          compute_d(kJL);
+          update_z(kJL, kLo);
           update_r(kLo);
           int l = 0;
           double t1 = inf;
@@ -824,7 +832,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
               if (k < IQLO || k < iq) uv[k] -= t * rv[k];
             lput_lo<IQLO>(uv, iq, lsel_lo<IQLO>(uv, iq) + t);
             act &= ~(1ull << l);
-            delete_constraint(l, kLo);
+            delete_constraint(l, kJL, kLo);
             need_scan = need_select = false;
           } else {
 #pragma unroll
@@ -835,9 +843,9 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
               if (k < IQLO || k < iq) uv[k] -= t * rv[k];
             lput_lo<IQLO>(uv, iq, lsel_lo<IQLO>(uv, iq) + t);
             if (fabs(t - t2) < kEps) {  // full step
-              if (!add_constraint(kLds, kLo)) {
+              if (!add_constraint(kJL, kLo)) {
                 excl |= 1ull << ip;
-                delete_constraint(ip, kLo);
+                delete_constraint(ip, kJL, kLo);
                 act = 0;
 #pragma unroll
                 for (int i = 0; i < NM; i++)
@@ -856,7 +864,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
               }
             } else {  // partial step: drop l, refresh s[ip] = CI[:,ip]^T x + ci0[ip]
               act &= ~(1ull << l);
-              delete_constraint(l, kLo);
+              delete_constraint(l, kJL, kLo);
               double s = 0.0;
 #pragma unroll
               for (int j = 0; j < NM; j++)
