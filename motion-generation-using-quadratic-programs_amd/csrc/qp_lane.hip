@@ -74,6 +74,10 @@ constexpr int kScanDepth = QPGPU_SCAN_DEPTH;
 #ifndef QPGPU_LANE_JREG_LOOP
 #define QPGPU_LANE_JREG_LOOP 2
 #endif
+// rows of CI each lane keeps in LDS for the l1 scans (0 disables; see the LDS regions)
+#ifndef QPGPU_LANE_CI_LDS
+#define QPGPU_LANE_CI_LDS 1
+#endif
 // warm the caches with this lane's CI / ci0 lines before the equality phase (QP-major layout).
 // Off by default: measured (profiles/r01_s2/lane_ci_warmup.log) it shortens the mean wave (scan
 // 36k -> 28k cycles) but lowers the pipelined throughput ~4 % on C1 and C2 — the extra
@@ -91,6 +95,7 @@ __device__ __forceinline__ bool wave_any(bool v) { return __builtin_amdgcn_ballo
 // [p, iq) loop of the active-set phase (for n = 7, p = 6 that range holds at most one entry).
 template <int NM, int MM, int T, bool EXACT, int QPW, int PX>
 __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const QpArgs a) {
+  constexpr bool kJregLoopCfg = QPGPU_LANE_JREG_LOOP == 2 || (QPGPU_LANE_JREG_LOOP == 1 && PX == 0);
   static_assert(QPW == 64 || (QPW == 32 && T == 1), "half waves only with the QP-major layout");
   static_assert(MM <= 64, "bitmask bookkeeping holds m <= 64");
   using RI = RIdx<NM>;
@@ -155,14 +160,20 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
 #pragma unroll
   for (int i = 0; i < NM; i++) xv[i] = 0.0;
   double c1 = 0.0, c2 = 0.0;
-  // LDS regions: JA = J (lane-interleaved, element (i,j) of lane l at [(i*NM+j)*64 + l]),
-  // which first serves as the staging area for G and then CE; RB = g0 staging, then the
-  // rollback copies x_old / u_old / A_old.  Keeping J and the rollback state out of VGPRs
-  // leaves the compiler room to keep memory operations in flight.
+  // LDS regions: the bottom of the buffer stages G (setup), then CE / ce0 (equality phase),
+  // then — when J stays in registers — rows 0..kCiRows-1 of every lane's CI for the active-set
+  // loop (16-B pieces, piece k of lane l at doubles (k*QPW + l)*2); otherwise it holds J's LDS
+  // image (element (i,j) of lane l at (i*NM+j)*QPW + l).  RB, at the top, = g0 staging, then
+  // the rollback copies x_old / u_old / A_old.
   constexpr int JA = (QPW * NM * NM + 127) / 128 * 128;
-  constexpr int RB = JA;
+  constexpr int RBSZ = QPW * NM + 2 * QPW * (NM + 1);
+  constexpr int RB = (STAGE - RBSZ) / 2 * 2;
   constexpr int RB_U = RB + QPW * NM, RB_A = RB_U + QPW * (NM + 1);
-  static_assert(RB_A + QPW * (NM + 1) <= STAGE, "LDS regions exceed the stage buffer");
+  static_assert(RB >= JA && RB >= QPW * NM * NM, "LDS regions exceed the stage buffer");
+  // CI rows held in LDS through the loop (EXACT QP-major shapes, J in registers)
+  constexpr int kCiRowsFit = (RB / QPW) / MM;
+  constexpr int kCiRows = (EXACT && T == 1 && kJregLoopCfg && MM % 2 == 0)
+                              ? (kCiRowsFit < NM ? kCiRowsFit : NM) : 0;
 #define Jr_(i, j) sbuf[((i) * NM + (j)) * QPW + lane]
   // J lives in registers (compile-time indices) through the J build and the equality phase,
   // where every step reads and rotates all of it; the loop then works on its LDS image.  CE
@@ -171,7 +182,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   bool ce_staged = false;
   // keep J in registers through the active-set loop too (QPGPU_LANE_JREG_LOOP: 0 never, 1 when
   // p = 0 — no equality phase, the loop does all the rotations — , 2 always)
-  constexpr bool kJregLoop = QPGPU_LANE_JREG_LOOP == 2 || (QPGPU_LANE_JREG_LOOP == 1 && PX == 0);
+  constexpr bool kJregLoop = kJregLoopCfg;
   // one dword per 128-B line of this lane's CI / ci0 blocks (cache warm-up, see below)
   constexpr int kPfCI = (NM * MM * 8 + 127) / 128 + 1, kPfC0 = (MM * 8 + 127) / 128 + 1;
   [[maybe_unused]] uint32_t pf[kPfCI + kPfC0];
@@ -607,6 +618,14 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
 #pragma unroll
       for (int j = 0; j < NM; j++) Jr_(i, j) = Jreg[i][j];
   }
+  // CI rows 0..kCiRows-1 are kept in LDS for the loop: the first l1 scan (which every active
+  // lane runs, loading those rows into registers anyway) writes them there, so each later scan
+  // issues only the remaining rows' global loads and the selected-column gather takes those
+  // rows from LDS — no extra global traffic and nothing to wait for.
+  const bool ci_lds = QPGPU_LANE_CI_LDS && kCiRows > 0 && (a.flags & kArgAligned16);
+  bool ci_ready = false;  // wave-uniform: the LDS copy has been written
+  // element e (= row * MM + column) of this lane's CI from the LDS copy (e < kCiRows * MM)
+  auto ci_lds_at = [&](int e) -> double { return sbuf[((e >> 1) * QPW + lane) * 2 + (e & 1)]; };
   qp_stamp(a, 2);
 
   // ---------------------------------------------------------------- active-set loop
@@ -708,9 +727,19 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
           // in rowbuf[r % D], issued D-1 rows ahead of its use
           constexpr int D = kScanDepth;
           double rowbuf[D][MM];
+          const bool from_lds = ci_lds && ci_ready;
+          const bool fill_lds = ci_lds && !ci_ready;
           auto load_row = [&](int r, double* dst) {
             if (r < NM) {
-              if (r < n) {
+              if (r < kCiRows && from_lds) {
+#pragma unroll
+                for (int i = 0; i < MM; i += 2) {
+                  const double2 v =
+                      *reinterpret_cast<const double2*>(sbuf + (((r * MM + i) >> 1) * QPW + lane) * 2);
+                  dst[i] = v.x;
+                  dst[i + 1] = v.y;
+                }
+              } else if (r < n) {
                 if constexpr (T == 1)
                   ldrow(dst, CIg + r * m);
                 else
@@ -736,6 +765,12 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
 #pragma unroll
               for (int i = 0; i < MM; i++)
                 if (i < m) sv[i] += rowbuf[j % D][i] * xj;
+              if (j < kCiRows && fill_lds) {
+#pragma unroll
+                for (int i = 0; i < MM; i += 2)
+                  *reinterpret_cast<double2*>(sbuf + (((j * MM + i) >> 1) * QPW + lane) * 2) =
+                      double2{rowbuf[j % D][i], rowbuf[j % D][i + 1]};
+              }
             }
             __builtin_amdgcn_sched_barrier(0);
           }
@@ -746,6 +781,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
               psi += (sv[i] < 0.0) ? sv[i] : 0.0;
             }
         }
+        ci_ready = ci_lds;
         if (do_scan) {
           excl = 0;
           ss = 0.0;
@@ -779,7 +815,8 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
           active = false;  // optimal
         } else {
 #pragma unroll
-          for (int j = 0; j < NM; j++) npv[j] = (j < n) ? ldCI(j * m + ip) : 0.0;
+          for (int j = 0; j < NM; j++)
+            npv[j] = (j < n) ? ((j < kCiRows && ci_ready) ? ci_lds_at(j * MM + ip) : ldCI(j * m + ip)) : 0.0;
           ci0ip = ldci0(ip);
           lput_lo<IQLO>(uv, iq, 0.0);
           lput_lo<IQLO>(Av, iq, ip);
