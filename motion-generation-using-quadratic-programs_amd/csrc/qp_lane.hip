@@ -163,12 +163,11 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   // LDS regions: the bottom of the buffer stages G (setup), then CE / ce0 (equality phase),
   // then — when J stays in registers — rows 0..kCiRows-1 of every lane's CI for the active-set
   // loop (16-B pieces, piece k of lane l at doubles (k*QPW + l)*2); otherwise it holds J's LDS
-  // image (element (i,j) of lane l at (i*NM+j)*QPW + l).  RB, at the top, = g0 staging, then
-  // the rollback copies x_old / u_old / A_old.
+  // image (element (i,j) of lane l at (i*NM+j)*QPW + l).  RB, at the top, = g0 staging (the
+  // rollback copies x_old / u_old / A_old live in registers).
   constexpr int JA = (QPW * NM * NM + 127) / 128 * 128;
-  constexpr int RBSZ = QPW * NM + 2 * QPW * (NM + 1);
+  constexpr int RBSZ = QPW * NM;
   constexpr int RB = (STAGE - RBSZ) / 2 * 2;
-  constexpr int RB_U = RB + QPW * NM, RB_A = RB_U + QPW * (NM + 1);
   static_assert(RB >= JA && RB >= QPW * NM * NM, "LDS regions exceed the stage buffer");
   // CI rows held in LDS through the loop (EXACT QP-major shapes, J in registers)
   constexpr int kCiRowsFit = (RB / QPW) / MM;
@@ -641,9 +640,12 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
     double sv[MM];
 #pragma unroll
     for (int i = 0; i < MM; i++) sv[i] = 0.0;
-#define XOLD(i) sbuf[RB + (i) * QPW + lane]
-#define UOLD(i) sbuf[RB_U + (i) * QPW + lane]
-#define AOLD(i) sbuf[RB_A + (i) * QPW + lane]
+    // rollback copies (compile-time indices only: registers)
+    double xold_r[NM], uold_r[NM];
+    int aold_r[NM];
+#define XOLD(i) xold_r[i]
+#define UOLD(i) uold_r[i]
+#define AOLD(i) aold_r[i]
     uint64_t act = 0;   // bit c set <=> iai[c] == -1
     uint64_t excl = 0;  // bit c set <=> iaexcl[c] == false
     int ip = 0, steps = 0;
@@ -793,7 +795,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
             for (int i = 0; i < NM; i++) {
               if (i < IQLO || i < iq) {
                 UOLD(i) = uv[i];
-                AOLD(i) = (double)Av[i];
+                AOLD(i) = Av[i];
               }
               XOLD(i) = xv[i];
             }
