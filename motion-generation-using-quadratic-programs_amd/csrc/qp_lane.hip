@@ -74,6 +74,13 @@ constexpr int kScanDepth = QPGPU_SCAN_DEPTH;
 #ifndef QPGPU_LANE_JREG_LOOP
 #define QPGPU_LANE_JREG_LOOP 2
 #endif
+// where the active-set loop keeps the rollback copies x_old / u_old / A_old: 0 LDS, 1 registers
+// when p > 0 (LDS for p = 0, whose loop already holds J and the Givens state in registers),
+// 2 registers always.  Measured: 2 vs 0 on C1 58.4 -> 49.4 us (lane_rollback_regs.log); 1 vs
+// 2 on C2 within noise (c2_rollback_lds_*.log, 170 vs 239 AGPRs), so 2 serves both
+#ifndef QPGPU_LANE_RB_REGS
+#define QPGPU_LANE_RB_REGS 2
+#endif
 // rows of CI each lane keeps in LDS for the l1 scans (0 disables; see the LDS regions)
 #ifndef QPGPU_LANE_CI_LDS
 #define QPGPU_LANE_CI_LDS 1
@@ -96,6 +103,7 @@ __device__ __forceinline__ bool wave_any(bool v) { return __builtin_amdgcn_ballo
 template <int NM, int MM, int T, bool EXACT, int QPW, int PX>
 __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const QpArgs a) {
   constexpr bool kJregLoopCfg = QPGPU_LANE_JREG_LOOP == 2 || (QPGPU_LANE_JREG_LOOP == 1 && PX == 0);
+  constexpr bool kRbRegs = QPGPU_LANE_RB_REGS == 2 || (QPGPU_LANE_RB_REGS == 1 && PX != 0);
   static_assert(QPW == 64 || (QPW == 32 && T == 1), "half waves only with the QP-major layout");
   static_assert(MM <= 64, "bitmask bookkeeping holds m <= 64");
   using RI = RIdx<NM>;
@@ -163,11 +171,12 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   // LDS regions: the bottom of the buffer stages G (setup), then CE / ce0 (equality phase),
   // then — when J stays in registers — rows 0..kCiRows-1 of every lane's CI for the active-set
   // loop (16-B pieces, piece k of lane l at doubles (k*QPW + l)*2); otherwise it holds J's LDS
-  // image (element (i,j) of lane l at (i*NM+j)*QPW + l).  RB, at the top, = g0 staging (the
-  // rollback copies x_old / u_old / A_old live in registers).
+  // image (element (i,j) of lane l at (i*NM+j)*QPW + l).  RB, at the top, = g0 staging, then
+  // (unless they live in registers, kRbRegs) the rollback copies x_old / u_old / A_old.
   constexpr int JA = (QPW * NM * NM + 127) / 128 * 128;
-  constexpr int RBSZ = QPW * NM;
+  constexpr int RBSZ = QPW * NM + (kRbRegs ? 0 : 2 * QPW * (NM + 1));
   constexpr int RB = (STAGE - RBSZ) / 2 * 2;
+  constexpr int RB_U = RB + QPW * NM, RB_A = RB_U + QPW * (NM + 1);
   static_assert(RB >= JA && RB >= QPW * NM * NM, "LDS regions exceed the stage buffer");
   // CI rows held in LDS through the loop (EXACT QP-major shapes, J in registers)
   constexpr int kCiRowsFit = (RB / QPW) / MM;
@@ -640,12 +649,12 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
     double sv[MM];
 #pragma unroll
     for (int i = 0; i < MM; i++) sv[i] = 0.0;
-    // rollback copies (compile-time indices only: registers)
-    double xold_r[NM], uold_r[NM];
-    int aold_r[NM];
-#define XOLD(i) xold_r[i]
-#define UOLD(i) uold_r[i]
-#define AOLD(i) aold_r[i]
+    // rollback copies: registers (compile-time indices only) or lane-interleaved LDS
+    [[maybe_unused]] double xold_r[NM], uold_r[NM];
+    [[maybe_unused]] int aold_r[NM];
+#define XOLD(i) (*(kRbRegs ? &xold_r[i] : &sbuf[RB + (i) * QPW + lane]))
+#define UOLD(i) (*(kRbRegs ? &uold_r[i] : &sbuf[RB_U + (i) * QPW + lane]))
+#define AOLD(i) (*(kRbRegs ? &aold_r[i] : reinterpret_cast<int*>(&sbuf[RB_A + (i) * QPW + lane])))
     uint64_t act = 0;   // bit c set <=> iai[c] == -1
     uint64_t excl = 0;  // bit c set <=> iaexcl[c] == false
     int ip = 0, steps = 0;

@@ -1,0 +1,196 @@
+// eigen_api_test.cpp — exercises the Eigen-variant drop-in (include/quadprog_amd/eigen/
+// QuadProg++.hh: QuadProgpp::Solver::solve -> Status, reference eigen/QuadProg++.hh:83-118)
+// against the ArrayHH drop-in solve_quadprog (libquadprog_amd.so) on the same problems.
+// Eigen is not installed here, so the Eigen code path is exercised through an Eigen-like
+// column-major matrix type (rows()/cols()/operator()(i, j)) instantiating the same template the
+// Eigen signature calls; the ArrayHH build of the header (QUADPROGPP_DISABLE_EIGEN) is the
+// Solver itself.  Built by __graft_entry__.build(); run by tests/test_gpu_dropin.py.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "QuadProg++.hh"
+#include "eigen/QuadProg++.hh"
+
+static int fails = 0;
+#define CHECK(c)                                               \
+  do {                                                         \
+    if (!(c)) {                                                \
+      std::printf("CHECK FAILED line %d: %s\n", __LINE__, #c); \
+      fails++;                                                 \
+    }                                                          \
+  } while (0)
+
+static bool same_bits(double a, double b) { return std::memcmp(&a, &b, 8) == 0; }
+
+// Eigen-like dense column-major containers (the access pattern of Eigen::MatrixXd/VectorXd)
+struct ColMat {
+  unsigned r = 0, c = 0;
+  std::vector<double> v;
+  ColMat(unsigned r_ = 0, unsigned c_ = 0) : r(r_), c(c_), v((size_t)r_ * c_, 0.0) {}
+  long rows() const { return r; }
+  long cols() const { return c; }
+  double& operator()(unsigned i, unsigned j) { return v[(size_t)j * r + i]; }
+  const double& operator()(unsigned i, unsigned j) const { return v[(size_t)j * r + i]; }
+};
+struct ColVec {
+  std::vector<double> v;
+  explicit ColVec(unsigned n = 0) : v(n, 0.0) {}
+  long size() const { return (long)v.size(); }
+  void resize(unsigned n) { v.resize(n); }
+  double& operator[](unsigned i) { return v[i]; }
+  const double& operator[](unsigned i) const { return v[i]; }
+};
+
+// deterministic pseudo-random problem: G SPD (diagonally dominant), p equalities, m inequalities
+struct Prob {
+  unsigned n, p, m;
+  std::vector<double> G, g0, CE, ce0, CI, ci0;  // row-major n x n, n x p, n x m
+};
+static Prob make(unsigned n, unsigned p, unsigned m, unsigned seed, bool infeasible) {
+  Prob P{n, p, m, {}, {}, {}, {}, {}, {}};
+  uint64_t s = 0x9E3779B97F4A7C15ull * (seed + 1);
+  auto rnd = [&]() {
+    s ^= s << 13;
+    s ^= s >> 7;
+    s ^= s << 17;
+    return (double)(s >> 11) / 9007199254740992.0 * 2.0 - 1.0;
+  };
+  std::vector<double> A((size_t)n * n);
+  for (auto& a : A) a = rnd();
+  P.G.assign((size_t)n * n, 0.0);
+  for (unsigned i = 0; i < n; i++)
+    for (unsigned j = 0; j < n; j++) {
+      double t = 0.0;
+      for (unsigned k = 0; k < n; k++) t += A[i * n + k] * A[j * n + k];
+      P.G[i * n + j] = t + (i == j ? 0.5 * n : 0.0);
+    }
+  for (unsigned i = 0; i < n; i++) P.g0.push_back(rnd());
+  for (unsigned i = 0; i < n * p; i++) P.CE.push_back(rnd());
+  for (unsigned i = 0; i < n * m; i++) P.CI.push_back(rnd());
+  // feasible by construction: xf satisfies the equalities and every inequality with slack
+  std::vector<double> xf(n);
+  for (auto& v : xf) v = rnd();
+  for (unsigned j = 0; j < p; j++) {
+    double s = 0.0;
+    for (unsigned i = 0; i < n; i++) s += P.CE[i * p + j] * xf[i];
+    P.ce0.push_back(-s);
+  }
+  for (unsigned j = 0; j < m; j++) {
+    double s = 0.0;
+    for (unsigned i = 0; i < n; i++) s += P.CI[i * m + j] * xf[i];
+    P.ci0.push_back(-s + 0.1 + 0.5 * (rnd() + 1.0));
+  }
+  if (infeasible) {  // x0 >= 1 and -x0 >= 1
+    for (unsigned i = 0; i < n; i++) P.CI[i * m + 0] = P.CI[i * m + 1] = 0.0;
+    P.CI[0 * m + 0] = 1.0;
+    P.CI[0 * m + 1] = -1.0;
+    P.ci0[0] = P.ci0[1] = -1.0;
+  }
+  return P;
+}
+
+int main() {
+  // 1. QuadProg++ demo through the Solver (ArrayHH containers): same bits as solve_quadprog;
+  //    G is left unchanged (the fork factors a copy)
+  {
+    QuadProgpp::Matrix<double> G(2, 2), CE(2, 1), CI(2, 3);
+    QuadProgpp::Vector<double> g0(2), ce0(1), ci0(3), x;
+    G[0][0] = 4; G[0][1] = -2; G[1][0] = -2; G[1][1] = 4;
+    g0[0] = 6; g0[1] = 0;
+    CE[0][0] = 1; CE[1][0] = 1; ce0[0] = -3;
+    CI[0][0] = 1; CI[0][1] = 0; CI[0][2] = 1; CI[1][0] = 0; CI[1][1] = 1; CI[1][2] = 1;
+    ci0[0] = 0; ci0[1] = 0; ci0[2] = -2;
+    QuadProgpp::Solver qp;
+    CHECK(qp.solve(G, g0, CE, ce0, CI, ci0, x) == QuadProgpp::Status::OK);
+    CHECK(x.size() == 2);
+    CHECK(qp.objective() == 12.0);
+    CHECK(same_bits(x[0], 1.0));
+    CHECK(same_bits(x[1], 2.0000000000000009));
+    CHECK(G[0][0] == 4.0 && G[0][1] == -2.0 && G[1][0] == -2.0 && G[1][1] == 4.0);
+  }
+  // 2. random problems: Solver (ArrayHH), the Eigen-like column-major path and solve_quadprog
+  //    agree bit for bit (x, cost); infeasible problems give FAILURE
+  QuadProgpp::Solver qp;  // one solver reused across calls (its staging is reused)
+  int solved = 0, infeasible = 0;
+  for (unsigned t = 0; t < 24; t++) {
+    const unsigned n = 2 + t % 7, p = (t % 3 == 0) ? 0 : (t % n), m = 2 * n + t % 5;
+    const bool infeas = (t % 6 == 5);
+    const Prob P = make(n, p, m, t, infeas);
+    ArrayHH::Matrix<double> Ga(n, n), CEa(n, p), CIa(n, m);
+    ArrayHH::Vector<double> g0a(n), ce0a(p), ci0a(m), xa;
+    QuadProgpp::Matrix<double> Gs(n, n), CEs(n, p), CIs(n, m);
+    QuadProgpp::Vector<double> g0s(n), ce0s(p), ci0s(m), xs;
+    ColMat Gc(n, n), CEc(n, p), CIc(n, m);
+    ColVec g0c(n), ce0c(p), ci0c(m), xc;
+    for (unsigned i = 0; i < n; i++) {
+      for (unsigned j = 0; j < n; j++) Ga[i][j] = Gs[i][j] = Gc(i, j) = P.G[i * n + j];
+      for (unsigned j = 0; j < p; j++) CEa[i][j] = CEs[i][j] = CEc(i, j) = P.CE[i * p + j];
+      for (unsigned j = 0; j < m; j++) CIa[i][j] = CIs[i][j] = CIc(i, j) = P.CI[i * m + j];
+      g0a[i] = g0s[i] = g0c[i] = P.g0[i];
+    }
+    for (unsigned j = 0; j < p; j++) ce0a[j] = ce0s[j] = ce0c[j] = P.ce0[j];
+    for (unsigned j = 0; j < m; j++) ci0a[j] = ci0s[j] = ci0c[j] = P.ci0[j];
+    double fa;
+    bool threw = false;
+    try {
+      fa = solve_quadprog(Ga, g0a, CEa, ce0a, CIa, ci0a, xa);
+    } catch (const std::exception&) {  // dependent equalities: a FAILURE for the Solver
+      threw = true;
+      fa = std::numeric_limits<double>::quiet_NaN();
+    }
+    const QuadProgpp::Status::Value st = qp.solve(Gs, g0s, CEs, ce0s, CIs, ci0s, xs);
+    const double fs = qp.objective();
+    QuadProgpp::amd_detail::Staging stg;
+    double fc = 0.0;
+    const int stc = QuadProgpp::amd_detail::solve_generic(stg, Gc, g0c, CEc, ce0c, CIc, ci0c, xc, fc);
+    const bool ok = !threw && std::isfinite(fa);
+    CHECK((st == QuadProgpp::Status::OK) == ok);
+    CHECK((stc == QPGPU_QP_OK) == ok);
+    if (infeas) CHECK(!ok && std::isinf(fs) && stc == QPGPU_QP_INFEASIBLE);
+    if (ok) {
+      solved++;
+      CHECK(same_bits(fa, fs) && same_bits(fa, fc));
+      for (unsigned i = 0; i < n; i++) CHECK(same_bits(xa[i], xs[i]) && same_bits(xa[i], xc[i]));
+    } else if (!threw) {
+      infeasible++;
+    }
+    for (unsigned i = 0; i < n; i++)  // G untouched by the Solver and the generic path
+      for (unsigned j = 0; j < n; j++)
+        CHECK(same_bits(Gs[i][j], P.G[i * n + j]) && same_bits(Gc(i, j), P.G[i * n + j]));
+  }
+  std::printf("random problems: %d solved, %d infeasible\n", solved, infeasible);
+  CHECK(solved >= 12 && infeasible >= 4);
+  // 3. G not positive definite: FAILURE (no exception), objective() = the failing pivot
+  {
+    QuadProgpp::Matrix<double> G(2, 2), CE(2, 0), CI(2, 0);
+    QuadProgpp::Vector<double> g0(2), ce0(0), ci0(0), x;
+    G[0][0] = 1; G[0][1] = 2; G[1][0] = 2; G[1][1] = 1;
+    g0[0] = 0; g0[1] = 0;
+    CHECK(qp.solve(G, g0, CE, ce0, CI, ci0, x) == QuadProgpp::Status::FAILURE);
+    CHECK(qp.detailed_status() == QPGPU_QP_NOT_POSITIVE_DEFINITE);
+    CHECK(qp.objective() == -3.0);
+  }
+  // 4. inconsistent dimensions: solve_quadprog's logic_error messages
+  {
+    QuadProgpp::Matrix<double> G(2, 2), CE(3, 1), CI(2, 0);
+    QuadProgpp::Vector<double> g0(2), ce0(1), ci0(0), x;
+    std::string what;
+    try {
+      qp.solve(G, g0, CE, ce0, CI, ci0, x);
+    } catch (const std::logic_error& e) {
+      what = e.what();
+    }
+    CHECK(what == "The matrix CE is incompatible (incorrect number of rows 3 , expecting 2)");
+  }
+  if (fails) {
+    std::printf("eigen_api_test: %d FAILED\n", fails);
+    return 1;
+  }
+  std::printf("eigen_api_test: OK\n");
+  return 0;
+}

@@ -35,6 +35,19 @@ def test_dropin_exports_reference_symbol():
     assert "_Z14solve_quadprogRN7ArrayHH6MatrixIdEERNS_6VectorIdEERKS1_RKS4_S7_S9_S5_" in out
 
 
+def test_eigen_api_header_builds_and_fails_loudly_without_gpu():
+    """QuadProgpp::Solver (reference eigen/QuadProg++.hh:83-118): build() compiled the test
+    program against the header; with no device it must abort on the C-ABI error, never solve
+    on the CPU."""
+    b = os.path.join(ROOT, "tests", "_build", "eigen_api_test")
+    assert os.path.exists(b), "build() did not produce tests/_build/eigen_api_test"
+    if qpgpu.device_count() > 0:
+        pytest.skip("a GPU is visible: covered by tests/test_gpu_dropin.py")
+    r = subprocess.run([b], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "qpgpu: solve failed" in r.stderr
+
+
 def test_kernel_coverage_table():
     assert qpgpu.kernel_name(7, 6, 14) != ""
     assert qpgpu.kernel_name(7, 0, 14) != ""
