@@ -2,78 +2,113 @@
 """Benchmark: batched Goldfarb–Idnani QP solves on MI355X (BASELINE.json metric).
 
 One "step" = one batched solve (one launch of the gfx950 kernel through the C-ABI
-qpgpu_solve_batched) over the rank's resident batch of synthetic QPs.  With N > 1 every rank
-solves its own shard (weak scaling, no data-path collective: the QPs are independent);
---gather adds an RCCL gather of each step's results (x, f, status) to rank 0 on a separate
-stream, overlapped with the following solves, for deployments that collect results centrally.  Inputs are
-generated on the host from the counter-based generator (qpgpu.make_problems) and copied to HBM
-before timing.
+qpgpu_solve_batched) over one resident batch of synthetic QPs per rank.
 
-Steps are independent batches (one control period's QPs each), so they are pipelined: step k is
-enqueued on HIP stream k mod S (--streams, default 3: GPU_MAX_HW_QUEUES is 4 and a fourth
-stream measured sharing a hardware queue) with its own output buffers.  With 65 536
-QPs a launch is exactly one wave per SIMD, so a single launch ends with most SIMDs idle behind
-its slowest waves; the next step's waves fill them.  `value` is the pipelined whole-job
-throughput; `roofline` uses the kernel's own duration from a separate serialized pass (HIP events
-around each launch, one stream), which is what `rocprofv3 ... bench.py --streams 1` reports.
+Workloads (--config; default C1 at N = 1 — the metric config — and C4 at N > 1):
+  C1   65 536 x (n=7, p=6, m=14) per GPU (weak scaling)
+  C4   1 048 576 x (7, 6, 14) GLOBAL, split into N contiguous shards (131 072 per GPU at N = 8)
+  C2, C3, mgqp, C5: the other BASELINE shapes on one GPU (parity-test configs, extra lines).
+With N > 1 each rank solves its own shard (the QPs are independent) and every
+step's results (x, f, status: 68 B per QP at n = 7) are gathered to rank 0 with ONE RCCL gather
+issued on a communication stream, overlapped with the following steps' solves (--no-gather
+turns it off).  `gather_ms` reports one step's gather alone, timed after the run.
 
-Default workload = BASELINE.json's metric config: 65 536 x (n=7, p=6, m=14) per GPU (weak
-scaling: per-GPU work is fixed as N grows; C4's 1M QPs on 8 GPUs is --batch 131072 --gpus 8).
+Cold inputs: a step reads its whole batch from HBM.  The rank keeps R >= 3 distinct resident
+input sets whose total exceeds twice the 256 MiB Infinity Cache when one set is smaller than it
+(set r = set 0 rotated by r*B/R QPs, copied to its own buffers) and steps rotate over them, so no
+step finds its inputs in the Infinity Cache (MI355X_MICROARCH.md: a table stays resident only
+while it plus everything touched between two uses fits in ~256 MiB).  The warm figure (one set
+re-solved) is reported beside it.
 
-Single-GPU:  python bench.py [--steps K --warmup W]
-Multi-GPU:   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Timing: steps are independent batches, pipelined round-robin over --streams HIP streams (default
+3) with private outputs; `value` is that whole-job throughput.  `value_streams1` is the same K
+steps serialized on one stream.  `roofline` uses the kernel's own duration: serialized launches
+on one stream bracketed by HIP events on that stream (cold rotation), which is what
+`rocprofv3 --kernel-trace --stats -- python bench.py --streams 1` reports.
+
+Single-GPU:  python bench.py [--steps K --warmup W] [--config C1|C2|C3|C4|mgqp|C5]
+Multi-GPU:   python bench.py --gpus N ...   (starts torch.distributed.run with N ranks itself)
+             python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(ROOT, "motion-generation-using-quadratic-programs_amd"))
+PKG = os.path.join(ROOT, "motion-generation-using-quadratic-programs_amd")
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-
-import qpdist  # noqa: E402
-import qpgpu  # noqa: E402
-
-METRIC = "QP solves/sec at n=7,p=6,m=14 batch=65536; achieved HBM GB/s vs peak"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MALL_BYTES = 256 << 20  # Infinity Cache
+C4_GLOBAL = 1 << 20
+# name: (kind, n, p, m, default batch per GPU (0 = C4 split), description)
 CONFIGS = {
-    # name: (kind, n, p, m, default batch per GPU, description)
-    "C1": ("general", 7, 6, 14, 65536, "C1/C4: 65536 x (n=7, p=6, m=14) general QPs per GPU"),
+    "C1": ("general", 7, 6, 14, 65536, "C1: 65536 x (n=7, p=6, m=14) general QPs per GPU"),
+    "C4": ("general", 7, 6, 14, 0, "C4: 1048576 x (n=7, p=6, m=14) general QPs split over the GPUs"),
     "C2": ("box", 7, 0, 14, 65536, "C2: 65536 x (n=7, p=0, m=14) joint-limit box QPs per GPU"),
     "C3": ("general", 30, 6, 60, 65536, "C3: 65536 x (n=30, p=6, m=60) general QPs per GPU"),
-    "mgqp": ("general", 14, 10, 28, 65536, "mgqp level-0 shape: 65536 x (n=14, p=10, m=28)"),
+    "mgqp": ("general", 14, 10, 28, 65536, "mgqp level-0 shape: 65536 x (n=14, p=10, m=28) per GPU"),
     "C5": ("general", 256, 0, 512, 4096, "C5: 4096 x (n=256, p=0, m=512) general QPs per GPU"),
 }
 
 
-def parse():
+def metric_name(cfg, n, p, m, B, world):
+    if cfg == "C1" and B == 65536:
+        return "QP solves/sec at n=7,p=6,m=14 batch=65536; achieved HBM GB/s vs peak"  # BASELINE.json
+    if cfg == "C4":
+        return (f"QP solves/sec at n=7,p=6,m=14 global batch={B * world} over {world} GPU(s); "
+                "achieved HBM GB/s vs peak")
+    return f"QP solves/sec at n={n},p={p},m={m} batch={B}; achieved HBM GB/s vs peak"
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="C1", choices=sorted(CONFIGS))
-    ap.add_argument("--batch", type=int, default=0, help="QPs per GPU (default: config's)")
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="workload (default: C1 on one GPU, C4 on N > 1)")
+    ap.add_argument("--batch", type=int, default=0, help="QPs per GPU (default: the config's)")
     ap.add_argument("--seed", type=int, default=2026)
     ap.add_argument("--family", default=None, choices=["lane", "subgroup", "wave"],
                     help="force a kernel family (default: the dispatcher's choice)")
     ap.add_argument("--layout", default="qp_major", choices=["qp_major", "tiled64"],
                     help="batch layout of the resident inputs (include/qpgpu.h)")
-    ap.add_argument("--gather", action="store_true",
-                    help="also gather every step's (x, f, status) to rank 0 over RCCL (N>1); off "
-                         "by default: the QPs are independent, so the path has no exchange step")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N > 1: skip the per-step RCCL gather of (x, f, status) to rank 0")
     ap.add_argument("--streams", type=int, default=3,
                     help="HIP streams the steps are pipelined over (1 = serialized launches)")
+    ap.add_argument("--input-sets", type=int, default=0,
+                    help="distinct resident input sets the steps rotate over (0 = enough to "
+                         "defeat the Infinity Cache, 1 = warm)")
     ap.add_argument("--kernel-reps", type=int, default=20,
                     help="serialized launches timed for the roofline's kernel duration")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(args):
+    """--gpus N > 1 outside torch.distributed.run: start it as a CHILD process (one rank per GPU)
+    before this process touches the GPU, pass rank 0's line through, exit with its code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4")))
 
 
 def cpu_baseline(pr, seconds):
@@ -122,20 +157,39 @@ def cpu_baseline(pr, seconds):
     return out
 
 
+def input_set_count(args, set_bytes):
+    if args.input_sets > 0:
+        return args.input_sets
+    if set_bytes >= 2 * MALL_BYTES:
+        return 1
+    return max(3, math.ceil(2 * MALL_BYTES / set_bytes))
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
+    if world != args.gpus:
+        sys.exit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    dist = None
-    # one rank per GPU; "nccl" is RCCL on ROCm.  QPGPU_DIST_BACKEND=gloo rehearses the N>1 flow
-    # with several ranks on one GPU (results then travel through host memory).
-    backend = os.environ.get("QPGPU_DIST_BACKEND", "nccl")
-    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+
+    sys.path.insert(0, PKG)
+    import numpy as np
+    import torch
+
+    import qpdist
+    import qpgpu
+
+    ndev = torch.cuda.device_count()  # does not initialise the GPU
+    # one rank per GPU, "nccl" = RCCL over xGMI.  Ranks sharing one GPU (a rehearsal on a 1-GPU
+    # box) cannot use RCCL, so they fall back to gloo (results then travel through host memory);
+    # QPGPU_DIST_BACKEND overrides.
+    backend = os.environ.get("QPGPU_DIST_BACKEND") or ("nccl" if ndev >= world else "gloo")
+    dev = torch.device("cuda", local % max(1, ndev))
     torch.cuda.set_device(dev)
+    dist = None
     if world > 1:
         import torch.distributed as dist
 
@@ -144,8 +198,16 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    kind, n, p, m, bdef, desc = CONFIGS[args.config]
-    B = args.batch or bdef
+    cfg = args.config or ("C1" if world == 1 else "C4")
+    kind, n, p, m, bdef, desc = CONFIGS[cfg]
+    if cfg == "C4" and not args.batch:
+        if C4_GLOBAL % world:
+            sys.exit(f"C4: {C4_GLOBAL} QPs do not split evenly over {world} ranks")
+        B = C4_GLOBAL // world
+        scaling = "strong"
+    else:
+        B = args.batch or bdef
+        scaling = "weak"
     b0, b1 = qpdist.shard(rank, B)
     pr = qpgpu.make_problems(kind, n, p, m, b0, b1, seed=args.seed)
     kname = qpgpu.kernel_name(n, p, m)
@@ -155,138 +217,186 @@ def main():
     if not kname:
         sys.exit(f"no gfx950 kernel covers (n, p, m) = {(n, p, m)}")
     base = qpgpu.DeviceBatch(pr, dev, with_iters=False, layout=args.layout)
+    bpq = qpgpu.algorithmic_bytes_per_qp(n, p, m)
+    in_bytes = 8 * (n * n + n + n * p + p + n * m + m)
+    R = input_set_count(args, in_bytes * B)
+    # set r = set 0 rotated by a whole number of 64-QP tiles (same flat roll in both layouts)
+    shifts = [(r * B // R) // 64 * 64 for r in range(R)]
+
+    def rotated(r):
+        s = base.__class__.__new__(base.__class__)
+        s.__dict__.update(base.__dict__)
+        for name, E in (("G", n * n), ("g0", n), ("CE", n * p), ("ce0", p), ("CI", n * m), ("ci0", m)):
+            t = getattr(base, name)
+            setattr(s, name, torch.roll(t.reshape(-1), shifts[r] * E).reshape(t.shape) if t.numel() else t.clone())
+        return s
+
+    sets = [base] + [rotated(r) for r in range(1, R)]
     S = max(1, args.streams)
-    gather = world > 1 and args.gather
-
-    def out_set():  # same resident inputs, private outputs
-        b = qpgpu.DeviceBatch.__new__(qpgpu.DeviceBatch)
-        b.__dict__.update(base.__dict__)
-        b.x = torch.empty_like(base.x)
-        b.f = torch.empty_like(base.f)
-        b.status = torch.empty_like(base.status)
-        return b
-
-    bufs = [base] + [out_set() for _ in range(S - 1)]
     streams = [torch.cuda.Stream(dev) for _ in range(S)]  # non-default streams (no implicit sync)
-    if gather:
-        rows = base.x.shape[0]
-        pdev = dev if backend == "nccl" else torch.device("cpu")
-        packed = [torch.empty((rows, n + 2), dtype=torch.float64, device=pdev) for _ in range(S)]
-        recv = [torch.empty((rows, n + 2), dtype=torch.float64, device=pdev) for _ in range(world)] if rank == 0 else None
-        comm = torch.cuda.Stream(dev)
-        works = [None] * S
+    outs = []
+    for _ in range(S):
+        outs.append((torch.empty_like(base.x), torch.empty_like(base.f), torch.empty_like(base.status)))
 
-    launch = [bufs[j].launcher(streams[j], family=args.family) for j in range(S)]
+    launchers = {}
 
-    def step(k):
-        j = k % S
-        db, cs = bufs[j], streams[j]
-        if gather and works[j] is not None:
-            # this stream's packed buffer is free once its gather finished: make stream cs
-            # wait for it (Work.wait() syncs the *current* stream with an nccl work)
-            with torch.cuda.stream(cs):
-                works[j].wait()
-            works[j] = None
-        launch[j]()
-        if gather:
-            # pack (x, f, status) and gather to rank 0 on the comm stream, overlapping the
-            # following steps' solves
-            pk = packed[j]
-            with torch.cuda.stream(cs):
-                if backend == "nccl":
-                    pk.copy_(qpdist.pack_results(db.x, db.f, db.status))
-                    done = torch.cuda.Event()
-                    done.record(cs)
-                    with torch.cuda.stream(comm):
-                        comm.wait_event(done)
-                        works[j] = dist.gather(pk, recv if rank == 0 else None, dst=0, async_op=True)
-                else:
-                    pk.copy_(qpdist.pack_results(db.x, db.f, db.status).cpu())
-                    works[j] = dist.gather(pk, recv if rank == 0 else None, dst=0, async_op=True)
+    def launcher(r, j, stream):
+        key = (r, j, stream.cuda_stream)
+        if key not in launchers:
+            v = sets[r].__class__.__new__(sets[r].__class__)
+            v.__dict__.update(sets[r].__dict__)
+            v.x, v.f, v.status = outs[j]
+            launchers[key] = v.launcher(stream, family=args.family)
+        return launchers[key]
 
-    for k in range(args.warmup):
-        step(k)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(args.warmup + k)
-    if gather:
-        for w in works:
-            if w is not None:
-                w.wait()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    # kernel-only duration for the roofline: serialized launches on one stream, HIP events
-    # bracketing each launch on the stream it runs on (untimed for `value`)
-    cs = streams[0]
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.kernel_reps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.kernel_reps)]
-    for r in range(args.kernel_reps):
-        starts[r].record(cs)
-        launch[0]()
-        ends[r].record(cs)
-    torch.cuda.synchronize(dev)
-    kern_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in zip(starts, ends)]))
-    if dist:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+    gather = world > 1 and not args.no_gather
+    gat = (qpdist.ResultGather(dist, rank, world, S, base.x.shape[0], n, dev, backend)
+           if gather else None)
 
-    st = bufs[0].status.cpu().numpy()
-    # every stream solved the same resident batch: identical outputs (guards the pipelining)
-    consistent = all(torch.equal(bufs[0].f, b_.f) and torch.equal(bufs[0].x, b_.x) for b_ in bufs[1:])
-    if rank != 0:
+    def step(k, S_=S):
+        j = k % S_
+        cs = streams[j]
+        if gat:
+            gat.wait(j, cs)  # slot j's record is free once its previous gather finished
+        launcher(k % R, j, cs)()
+        if gat:
+            gat.submit(j, *outs[j], stream=cs)
+
+    def sync_all():
+        if gat:
+            gat.drain()
+        torch.cuda.synchronize(dev)
         if dist:
-            dist.destroy_process_group()
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    def timed(K, W, S_):
+        for k in range(W):
+            step(k, S_)
+        sync_all()
+        t0 = time.perf_counter()
+        for k in range(K):
+            step(W + k, S_)
+        sync_all()
+        return time.perf_counter() - t0
+
+    elapsed = timed(args.steps, args.warmup, S)
+    # the last step of every stream slot, checked against set 0's solve rotated (guards the
+    # pipelining and the rotated sets): x, f, status bit for bit
+    last = {}
+    for k in range(args.warmup + args.steps - 1, args.warmup + args.steps - 1 - S, -1):
+        if k >= 0:
+            last[k % S] = k % R
+    ref_x, ref_f, ref_s = (t.clone() for t in outs[(args.warmup + args.steps - 1) % S])
+    ref_r = last[(args.warmup + args.steps - 1) % S]
+
+    def unrot(t, r, E):
+        return torch.roll(t.reshape(-1), -shifts[r] * E).reshape(t.shape)
+
+    consistent = True
+    if args.layout == "qp_major":
+        for j, r in last.items():
+            x_, f_, s_ = outs[j]
+            consistent &= bool(torch.equal(unrot(x_, r, n), unrot(ref_x, ref_r, n))
+                               and torch.equal(unrot(f_, r, 1), unrot(ref_f, ref_r, 1))
+                               and torch.equal(unrot(s_, r, 1), unrot(ref_s, ref_r, 1)))
+    st_ok = float((unrot(ref_s, ref_r, 1) == qpgpu.QP_OK).float().mean())
+    gather_ok = None
+    if gat and rank == 0:
+        # rank 0's own block of the last gather == what it packed, bit for bit
+        jl = (args.warmup + args.steps - 1) % S
+        gather_ok = bool(torch.equal(gat.received(jl)[0].cpu(), gat.packed[jl].cpu()))
+
+    # the same K steps on one stream (serialized launches)
+    elapsed1 = timed(args.steps, 0, 1) if S > 1 else elapsed
+
+    # kernel-only duration for the roofline: serialized launches on one stream, HIP events on
+    # that stream around each launch, rotating over the cold sets (and once more warm)
+    cs = streams[0]
+
+    def kernel_ms(rotate):
+        st_ = [torch.cuda.Event(enable_timing=True) for _ in range(args.kernel_reps)]
+        en_ = [torch.cuda.Event(enable_timing=True) for _ in range(args.kernel_reps)]
+        for q in range(args.kernel_reps):
+            fn = launcher(q % R if rotate else 0, 0, cs)
+            st_[q].record(cs)
+            fn()
+            en_[q].record(cs)
+        torch.cuda.synchronize(dev)
+        return float(np.mean([a_.elapsed_time(b_) for a_, b_ in zip(st_, en_)]))
+
+    kern_cold = kernel_ms(True)
+    kern_warm = kernel_ms(False)
+
+    gather_ms = gat.time_one() if gat else None  # one step's gather alone, same payload
+
+    if dist:
+        t = torch.tensor([elapsed, elapsed1, kern_cold, kern_warm, gather_ms or 0.0],
+                         dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, elapsed1, kern_cold, kern_warm = (float(v) for v in t[:4])
+        if gather:
+            gather_ms = float(t[4])
+        ok_t = torch.tensor([1 if consistent else 0], device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+        consistent = bool(ok_t.item())
+
+    if rank != 0:
+        dist.destroy_process_group()
         return
     total = B * world * args.steps
-    value = total / elapsed
-    bpq = qpgpu.algorithmic_bytes_per_qp(n, p, m)
-    achieved = bpq * B / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    traffic_src = None
+    achieved = bpq * B / (kern_cold * 1e-3) / 1e9
+    achieved_warm = bpq * B / (kern_warm * 1e-3) / 1e9
+    traffic = traffic_src = None
     try:
         tj = json.load(open(args.traffic_json))
-        key = f"{args.config}:{B}:{kname}"
+        key = f"{cfg}:{B}:{kname}"
         if key in tj:
             traffic = tj[key]["hbm_bytes_per_launch"]
             traffic_src = tj[key].get("source")
     except (OSError, ValueError):
         pass
+    par = f"batch-sharded x{world}"
+    if world > 1:
+        par += (f", {'RCCL' if backend == 'nccl' else backend} gather of (x, f, status) to rank 0 "
+                "per step (overlapped)" if gather else ", no collective")
     out = {
-        "metric": METRIC,
-        "value": value,
+        "metric": metric_name(cfg, n, p, m, B, world),
+        "value": total / elapsed,
         "unit": "QP solves/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
         "config": {"workload": desc, "kind": kind, "n": n, "p": p, "m": m, "batch_per_gpu": B,
                    "global_batch": B * world, "kernel": kname, "layout": args.layout,
-                   "streams": S,
-                   "parallelism": f"batch-sharded x{world}" + (", RCCL gather to rank 0 (overlapped)" if gather else ", no collective")},
+                   "streams": S, "input_sets": R, "cold_inputs": R > 1 or in_bytes * B >= 2 * MALL_BYTES,
+                   "backend": backend if world > 1 else None, "parallelism": par},
+        "value_streams1": total / elapsed1,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel_ms": kern_ms, "kernel_ms_source": "serialized launches, HIP events",
+                     "kernel_ms": kern_cold,
+                     "kernel_ms_source": "serialized launches on one stream, HIP events, inputs "
+                                         f"rotating over {R} resident set(s)",
+                     "warm": {"kernel_ms": kern_warm, "achieved": achieved_warm,
+                              "frac": achieved_warm / HBM_PEAK_GBS},
                      "algorithmic_bytes_per_qp": bpq,
                      "traffic_source": traffic_src},
-        "status_ok_frac": float((st == qpgpu.QP_OK).mean()),
-        "streams_outputs_identical": bool(consistent),
+        "status_ok_frac": st_ok,
+        "outputs_consistent": consistent,
     }
+    if gather:
+        out["gather_ms"] = gather_ms
+        out["gather_bytes_per_rank"] = gat.bytes_per_rank
+        out["gather_verified"] = gather_ok
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(pr, args.cpu_seconds)
-    print(json.dumps(out))
+    print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
 

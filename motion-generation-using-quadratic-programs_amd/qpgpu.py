@@ -337,14 +337,35 @@ def _normal(seed: int, idx: np.ndarray, stream: int, count: int) -> np.ndarray:
     return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * math.pi * u2)
 
 
-def make_problems(kind: str, n: int, p: int, m: int, b0: int, b1: int, seed: int = 2026) -> Problems:
+def make_problems(kind: str, n: int, p: int, m: int, b0: int, b1: int, seed: int = 2026,
+                  threads: int = 0) -> Problems:
     """Generate QPs [b0, b1) of a synthetic batch.
 
     kind="general" (C1, C3, C4, C5): G = M^T M + n I, g0 ~ 10 N(0,1), feasible point
         x_f ~ 0.1 N(0,1), CE ~ N(0,1), ce0 = -CE^T x_f, CI ~ N(0,1), ci0 = -CI^T x_f + |N(0,1)|.
     kind="box" (C2, mgqp joint-limit ordering, reference src/mgqp.cpp:1111-1112): same G, g0, CE;
         CI = [-I, +I] (m = 2n), ci0 = [hi; -lo] with hi = -lo = 1.
+
+    Every QP depends only on (seed, its global index), so large ranges are generated in chunks
+    on `threads` host threads (0 = up to 8; numpy releases the GIL) with identical results.
     """
+    B = b1 - b0
+    chunk = 8192
+    if threads == 0:
+        threads = min(8, os.cpu_count() or 1)
+    if threads > 1 and B > 2 * chunk:
+        from concurrent.futures import ThreadPoolExecutor
+
+        cuts = list(range(b0, b1, chunk)) + [b1]
+        with ThreadPoolExecutor(threads) as ex:
+            parts = list(ex.map(lambda c: _make_range(kind, n, p, m, c[0], c[1], seed),
+                                zip(cuts[:-1], cuts[1:])))
+        cat = lambda k: np.concatenate([getattr(q, k) for q in parts])
+        return Problems(n, p, m, cat("G"), cat("g0"), cat("CE"), cat("ce0"), cat("CI"), cat("ci0"))
+    return _make_range(kind, n, p, m, b0, b1, seed)
+
+
+def _make_range(kind: str, n: int, p: int, m: int, b0: int, b1: int, seed: int) -> Problems:
     idx = np.arange(b0, b1, dtype=np.uint64)
     B = b1 - b0
     M = _normal(seed, idx, 0, n * n).reshape(B, n, n)

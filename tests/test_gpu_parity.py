@@ -236,3 +236,12 @@ def test_eq_snapshot_equals_m0_solve(gpu, family, layout, kind, n, p, m):
     assert np.array_equal(fe.cpu().numpy().view(np.uint64), f0.view(np.uint64))
     ok = s0 != qpgpu.QP_NOT_POSITIVE_DEFINITE
     assert np.array_equal(xe[ok].view(np.uint64), x0[ok].view(np.uint64))
+
+
+def test_c4_shard_parity(gpu):
+    """One rank's shard of C4 (1 048 576 x (7, 6, 14) over 8 GPUs): the last rank's 131 072 QPs,
+    generated from their global indices as bench.py's rank 7 does, bitwise against the oracle."""
+    import qpdist
+
+    b0, b1 = qpdist.shard(7, 131072)
+    assert_parity(qpgpu.make_problems("general", 7, 6, 14, b0, b1, seed=2026), "C4 shard 7")

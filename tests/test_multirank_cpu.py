@@ -1,12 +1,16 @@
-"""World-size-2 test of the N>1 path on CPU (gloo): each rank generates only its shard from the
-counter-based generator, solves it (the oracle stands in for the GPU solve here, as test
-infrastructure), packs the results and gathers them to rank 0 with qpdist — rank 0 must hold
-exactly the single-process solution of the whole global batch."""
+"""World-size-2 tests of the N>1 path on CPU (gloo).
+
+Each rank generates only its shard from the counter-based generator, "solves" it (the oracle
+stands in for the GPU solve here, as test infrastructure), and pushes every step's results
+through qpdist.ResultGather — the same slot rotation bench.py drives (wait(j) before re-packing
+slot j, submit(j) packs and gathers asynchronously, drain() at the end).  Rank 0 must hold
+exactly the single-process solution of the whole global batch for every step, bit for bit."""
 import os
 import socket
 import sys
 
 import numpy as np
+import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
@@ -23,7 +27,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, per_rank, out_path):
+def _worker(rank, world, port, per_rank, steps, slots, out_path):
     sys.path[:0] = [PKG, os.path.join(ROOT, "oracle")]
     import torch
 
@@ -33,31 +37,71 @@ def _worker(rank, world, port, per_rank, out_path):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    b0, b1 = qpdist.shard(rank, per_rank)
-    pr = qpgpu.make_problems("general", 7, 6, 14, b0, b1, seed=2026)
-    x, f, st, _ = oracle.solve_batch(pr, max_steps=3700)
-    packed = torch.from_numpy(qpdist.pack_results(x, f, st))
-    _, recv = qpdist.gather_to_rank0(dist, packed, rank, world)
+    gat = qpdist.ResultGather(dist, rank, world, slots, per_rank, 7, "cpu", "gloo")
+    got = {}
+    for k in range(steps):
+        # step k solves the k-th global batch: rank r owns [k*W*P + r*P, k*W*P + (r+1)*P)
+        b0 = k * world * per_rank + rank * per_rank
+        pr = qpgpu.make_problems("general", 7, 6, 14, b0, b0 + per_rank, seed=2026, threads=1)
+        x, f, st, _ = oracle.solve_batch(pr, max_steps=3700)
+        j = k % slots
+        gat.wait(j)
+        if rank == 0 and k >= slots:  # slot j's previous gather has landed: keep it
+            got[k - slots] = qpdist.unpack_results(gat.received(j), 7, per_rank)
+        gat.submit(j, torch.from_numpy(x), torch.from_numpy(f), torch.from_numpy(st))
+    gat.drain()
     if rank == 0:
-        xg, fg, sg = qpdist.unpack_results(recv, 7, per_rank)
-        np.savez(out_path, x=xg, f=fg, s=sg)
+        for k in range(max(0, steps - slots), steps):
+            got[k] = qpdist.unpack_results(gat.received(k % slots), 7, per_rank)
+        np.savez(out_path, **{f"{a}{k}": v for k, t in got.items() for a, v in zip("xfs", t)})
+    ms = gat.time_one(reps=2)
+    assert ms > 0.0
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_shard_and_gather(tmp_path):
+@pytest.mark.parametrize("steps,slots", [(1, 1), (5, 3)])
+def test_two_rank_pipelined_gather(tmp_path, steps, slots):
     sys.path[:0] = [PKG, os.path.join(ROOT, "oracle")]
     import oracle
     import qpgpu
 
-    per_rank, world = 300, 2
+    per_rank, world = 200, 2
     out = str(tmp_path / "gathered.npz")
-    mp.start_processes(_worker, args=(world, _free_port(), per_rank, out), nprocs=world, join=True,
-                       start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), per_rank, steps, slots, out),
+                       nprocs=world, join=True, start_method="spawn")
     got = np.load(out)
-    full = qpgpu.make_problems("general", 7, 6, 14, 0, per_rank * world, seed=2026)
-    x, f, st, _ = oracle.solve_batch(full, max_steps=3700)
-    assert np.array_equal(got["x"], x) and np.array_equal(got["f"], f) and np.array_equal(got["s"], st)
+    for k in range(steps):
+        g0 = k * world * per_rank
+        full = qpgpu.make_problems("general", 7, 6, 14, g0, g0 + world * per_rank, seed=2026)
+        x, f, st, _ = oracle.solve_batch(full, max_steps=3700)
+        assert np.array_equal(got[f"x{k}"].view(np.uint64), x.view(np.uint64))
+        assert np.array_equal(got[f"f{k}"].view(np.uint64), f.view(np.uint64))
+        assert np.array_equal(got[f"s{k}"], st)
+
+
+def test_pack_roundtrip_is_bit_exact():
+    sys.path.insert(0, PKG)
+    import torch
+
+    import qpdist
+
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((70, 7))
+    x[3, 2] = np.nan
+    x[5, 0] = -0.0
+    f = rng.standard_normal(64)
+    f[1] = np.inf
+    st = rng.integers(0, 5, 64).astype(np.int32)
+    rec = qpdist.pack_results(x[:64], f, st)
+    assert rec.shape == (64, 17) and rec.dtype == np.int32  # 68 B per QP at n = 7
+    xb, fb, sb = qpdist.unpack_results([rec], 7, 64)
+    assert np.array_equal(xb.view(np.uint64), x[:64].view(np.uint64))
+    assert np.array_equal(fb.view(np.uint64), f.view(np.uint64)) and np.array_equal(sb, st)
+    # torch path with TILED64-padded x rows (padding rows carry f = status = 0)
+    out = torch.empty((70, 17), dtype=torch.int32)
+    qpdist.pack_results_into(out, torch.from_numpy(x), torch.from_numpy(f), torch.from_numpy(st))
+    assert np.array_equal(out.numpy()[:64], rec) and not out.numpy()[64:, 14:].any()
 
 
 def test_shard_ranges_tile_the_batch():
@@ -67,3 +111,20 @@ def test_shard_ranges_tile_the_batch():
     ranges = [qpdist.shard(r, 131072) for r in range(8)]
     assert ranges[0] == (0, 131072) and ranges[-1][1] == 8 * 131072  # C4: 1M QPs on 8 GPUs
     assert all(ranges[i][1] == ranges[i + 1][0] for i in range(7))
+
+
+def test_bench_c4_split_and_cold_sets():
+    """bench.py's workload arithmetic: C4 splits 1M QPs over N ranks; a C1 set is below the
+    Infinity Cache, so >= 3 sets totalling > 512 MiB rotate; a C4 shard at N = 2 is cold alone."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    a = bench.parse([])
+    c1 = 65536 * 8 * (49 + 7 + 42 + 6 + 98 + 14)
+    R = bench.input_set_count(a, c1)
+    assert R >= 3 and R * c1 > 2 * bench.MALL_BYTES
+    assert bench.input_set_count(a, (bench.C4_GLOBAL // 2) * c1 // 65536) == 1
+    assert bench.input_set_count(bench.parse(["--input-sets", "1"]), c1) == 1
+    assert bench.metric_name("C1", 7, 6, 14, 65536, 1).startswith("QP solves/sec at n=7,p=6,m=14 batch=65536")
+    assert "n=30" in bench.metric_name("C3", 30, 6, 60, 65536, 1)
+    assert "global batch=1048576 over 8" in bench.metric_name("C4", 7, 6, 14, 131072, 8)
