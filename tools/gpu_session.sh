@@ -45,7 +45,18 @@ for s in $STEPS; do
     stamps) for l in qp_major tiled64; do run stamps_general_$l 300 python tools/stamps.py general $l; run stamps_box_$l 300 python tools/stamps.py box $l; done ;;
     benchqpw)
       for q in 64 32; do QPGPU_LANE_QPW=$q run bench_qpw$q 600 python bench.py --family lane --no-cpu; done ;;
-    dist2) QPGPU_DIST_BACKEND=gloo run dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 ;;
+    dist2) run dist2 600 python bench.py --gpus 2 --steps 10 --warmup 2 ;;
+    dist2c1) run dist2c1 600 python bench.py --gpus 2 --config C1 --steps 10 --warmup 2 ;;
+    trace3) run trace3 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace3" -o c1 -- python3 bench.py --steps 20 --warmup 5 --no-cpu ;;
+    profC3) run profC3 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profC3" -o c3 -- python3 bench.py --config C3 --steps 5 --warmup 1 --no-cpu --streams 1 --kernel-reps 3 ;;
+    profC5) run profC5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profC5" -o c5 -- python3 bench.py --config C5 --steps 3 --warmup 1 --no-cpu --streams 1 --kernel-reps 2 ;;
+    pmcC5)
+      run pmcC5_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcC5_fetch" -o c5 -- python3 bench.py --config C5 --steps 2 --warmup 1 --no-cpu --streams 1 --kernel-reps 1
+      run pmcC5_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcC5_write" -o c5 -- python3 bench.py --config C5 --steps 2 --warmup 1 --no-cpu --streams 1 --kernel-reps 1
+      python3 tools/pmc_traffic.py "$OUT/pmcC5_fetch" "$OUT/pmcC5_write" C5 4096 "$(python3 -c 'import sys; sys.path.insert(0,"motion-generation-using-quadratic-programs_amd"); import qpgpu; print(qpgpu.kernel_name(256,0,512))')" "$OUT/pmc_traffic.json" ;;
+    benchcold)
+      for c in C1 C2 mgqp C3; do run benchcold_$c 600 python bench.py --config $c --no-cpu --steps 20; done
+      run benchcold_C5 600 python bench.py --config C5 --no-cpu --steps 3 --warmup 1 --kernel-reps 3 ;;
     listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;
     sq)
       for f in ${FAMILIES:-lane subgroup}; do
