@@ -1,0 +1,324 @@
+// mgqp_component.cpp — the reference's Orocos component on the RTT surface of
+// include/quadprog_amd/rtt/RTT.hh.  See include/quadprog_amd/mgqp_component.hh.
+#include "quadprog_amd/mgqp_component.hh"
+
+#include <iostream>
+#include <type_traits>
+
+namespace mgqp_amd {
+namespace rtt {
+
+namespace {
+std::string cat(const std::string& s, int i) { return s + std::to_string(i); }
+
+std::ostream& operator<<(std::ostream& os, const VecF& v) {  // Eigen's row-vector print
+  for (size_t i = 0; i < v.size(); ++i) os << (i ? " " : "") << v[i];
+  return os;
+}
+}  // namespace
+
+MotionGenerationQuadraticProgram::MotionGenerationQuadraticProgram(const std::string& name)
+    : RTT::TaskContext(name),
+      in_h_port("in_h_port"),
+      in_inertia_port("in_inertia_port"),
+      in_robotstatus_port("in_robotstatus_port"),
+      out_torques_port("out_torques_port"),
+      out_jointPosLimitInf_port("out_jointPosLimitInf"),
+      out_jointPosLimitSup_port("out_jointPosLimitSup"),
+      out_jointVelLimitInf_port("out_jointVelLimitInf"),
+      out_jointVelLimitSup_port("out_jointVelLimitSup"),
+      out_jointAccLimitInf_port("out_jointAccLimitInf"),
+      out_jointAccLimitSup_port("out_jointAccLimitSup"),
+      out_jointAccDynLimitInf_port("out_jointAccDynLimitInf"),
+      out_jointAccDynLimitSup_port("out_jointAccDynLimitSup"),
+      out_jointTorqueLimitInf_port("out_jointTorqueLimitInf"),
+      out_jointTorqueLimitSup_port("out_jointTorqueLimitSup") {
+  // src/mgqp.cpp:89-95
+  addOperation("setDOFsize", &MotionGenerationQuadraticProgram::setDOFsize, this, RTT::ClientThread)
+      .doc("set DOF size");
+  addOperation("setGains", &MotionGenerationQuadraticProgram::setGains, this, RTT::ClientThread)
+      .doc("set gains setGains(int kp, int kd)");
+  addOperation("printCurrentState", &MotionGenerationQuadraticProgram::printCurrentState, this,
+               RTT::ClientThread)
+      .doc("print current state");
+  addOperation("setAccelerationLimits", &MotionGenerationQuadraticProgram::setAccelerationLimits,
+               this, RTT::ClientThread)
+      .doc("set acceleration limits setAccelerationLimits(Eigen::VectorXf limitPositiv, "
+           "Eigen::VectorXf limitNegativ)");
+  addOperation("setTorqueLimits", &MotionGenerationQuadraticProgram::setTorqueLimits, this,
+               RTT::ClientThread)
+      .doc("set torque limits setTorqueLimits(Eigen::VectorXf limitPositiv, Eigen::VectorXf "
+           "limitNegativ)");
+  addOperation("setAngularLimits", &MotionGenerationQuadraticProgram::setAngularLimits, this,
+               RTT::ClientThread)
+      .doc("set angular limits setAngularLimits(Eigen::VectorXf limitSup, Eigen::VectorXf limitInf)");
+  addOperation("setPriorityLevel", &MotionGenerationQuadraticProgram::setPriorityLevel, this,
+               RTT::ClientThread)
+      .doc("set priority level of a task or it will be ignored");
+}
+
+template <class P>
+void MotionGenerationQuadraticProgram::clear(std::vector<P*>& v) {
+  for (P* p : v) delete p;
+  v.clear();
+}
+
+MotionGenerationQuadraticProgram::~MotionGenerationQuadraticProgram() { removeJointPorts(); }
+
+void MotionGenerationQuadraticProgram::removeJointPorts() {
+  for (int i = 1; i <= (int)DOFsize_ && portsPrepared_; ++i)
+    for (const char* s : {"in_jacobian_port_", "in_jacobianDot_port_", "in_currentTaskSpacePosition_port_",
+                          "in_currentTaskSpaceVelocity_port_", "in_currentTaskSpaceAcceleration_port_",
+                          "in_desiredTaskSpacePosition_port_", "in_desiredTaskSpaceVelocity_port_",
+                          "in_desiredTaskSpaceAcceleration_port_", "in_desiredJointSpacePosition_port_",
+                          "in_desiredJointSpaceVelocity_port_", "in_desiredJointSpaceAcceleration_port_"})
+      ports()->removePort(cat(s, i));
+  clear(in_desiredTaskSpacePosition_port);
+  clear(in_desiredTaskSpaceVelocity_port);
+  clear(in_desiredTaskSpaceAcceleration_port);
+  clear(in_currentTaskSpacePosition_port);
+  clear(in_currentTaskSpaceVelocity_port);
+  clear(in_currentTaskSpaceAcceleration_port);
+  clear(in_desiredJointSpacePosition_port);
+  clear(in_desiredJointSpaceVelocity_port);
+  clear(in_desiredJointSpaceAcceleration_port);
+  clear(in_jacobian_port);
+  clear(in_jacobianDot_port);
+}
+
+// src/mgqp.cpp:180-482: (re)creates every port; the per-joint ones are named with suffix 1..DOF
+void MotionGenerationQuadraticProgram::setDOFsize(unsigned int DOFsize) {
+  if (portsPrepared_) {
+    for (const char* s : {"in_robotstatus_port", "out_torques_port", "out_jointPosLimitInf",
+                          "out_jointPosLimitSup", "out_jointVelLimitInf", "out_jointVelLimitSup",
+                          "out_jointAccLimitInf", "out_jointAccLimitSup", "out_jointAccDynLimitInf",
+                          "out_jointAccDynLimitSup", "out_jointTorqueLimitInf", "out_jointTorqueLimitSup",
+                          "in_h_port", "in_inertia_port"})
+      ports()->removePort(s);
+    removeJointPorts();
+  }
+  DOFsize_ = DOFsize;
+  ctl_.setDOFsize(DOFsize);
+  for (int i = 1; i <= (int)DOFsize; ++i) {
+    in_desiredTaskSpacePosition_port.push_back(new RTT::InputPort<VecF>(cat("in_desiredTaskSpacePosition_port_", i)));
+    in_desiredTaskSpaceVelocity_port.push_back(new RTT::InputPort<VecF>(cat("in_desiredTaskSpaceVelocity_port_", i)));
+    in_desiredTaskSpaceAcceleration_port.push_back(new RTT::InputPort<VecF>(cat("in_desiredTaskSpaceAcceleration_port_", i)));
+    in_desiredJointSpacePosition_port.push_back(new RTT::InputPort<float>(cat("in_desiredJointSpacePosition_port_", i)));
+    in_desiredJointSpaceVelocity_port.push_back(new RTT::InputPort<float>(cat("in_desiredJointSpaceVelocity_port_", i)));
+    in_desiredJointSpaceAcceleration_port.push_back(new RTT::InputPort<float>(cat("in_desiredJointSpaceAcceleration_port_", i)));
+    in_currentTaskSpacePosition_port.push_back(new RTT::InputPort<VecF>(cat("in_currentTaskSpacePosition_port_", i)));
+    in_currentTaskSpaceVelocity_port.push_back(new RTT::InputPort<VecF>(cat("in_currentTaskSpaceVelocity_port_", i)));
+    in_currentTaskSpaceAcceleration_port.push_back(new RTT::InputPort<VecF>(cat("in_currentTaskSpaceAcceleration_port_", i)));
+    in_jacobian_port.push_back(new RTT::InputPort<MatF>(cat("in_jacobian_port_", i)));
+    in_jacobianDot_port.push_back(new RTT::InputPort<MatF>(cat("in_jacobianDot_port_", i)));
+  }
+  in_robotstatus_port.doc("Input port for reading robotstatus values");
+  ports()->addPort(in_robotstatus_port);
+  for (int i = 1; i <= (int)DOFsize; ++i) {
+    ports()->addPort(*in_jacobian_port[i - 1])
+        .doc(cat("Input port for receiving the Jacobian for joint", i) + "from fkin");
+    ports()->addPort(*in_jacobianDot_port[i - 1]).doc("Input port for receiving the EE JacobianDot from fkin");
+    ports()->addPort(*in_currentTaskSpacePosition_port[i - 1])
+        .doc("Input port for receiving the current task space position of the robot");
+    ports()->addPort(*in_currentTaskSpaceVelocity_port[i - 1])
+        .doc("Input port for receiving the current task space velocity of the robot");
+    ports()->addPort(*in_currentTaskSpaceAcceleration_port[i - 1])
+        .doc("Input port for receiving the current task space Acceleration of the robot");
+    ports()->addPort(*in_desiredTaskSpacePosition_port[i - 1])
+        .doc("to receive the position to track from a trajectory generator");
+    ports()->addPort(*in_desiredTaskSpaceVelocity_port[i - 1])
+        .doc("to receive the Velocity to track from a trajectory generator");
+    ports()->addPort(*in_desiredTaskSpaceAcceleration_port[i - 1])
+        .doc("to receive the Acceleration to track from a trajectory generator");
+    ports()->addPort(*in_desiredJointSpacePosition_port[i - 1])
+        .doc("to receive the angle to track from a trajectory generator");
+    ports()->addPort(*in_desiredJointSpaceVelocity_port[i - 1])
+        .doc("to receive the Velocity to track from a trajectory generator");
+    ports()->addPort(*in_desiredJointSpaceAcceleration_port[i - 1])
+        .doc("to receive the Acceleration to track from a trajectory generator");
+  }
+  ports()->addPort(in_h_port).doc("Input port to receive the weight, and coriolis matrix from fkin");
+  ports()->addPort(in_inertia_port).doc("Input port for the inertia Matrix");
+  out_torques_var = rstrt::dynamics::JointTorques((int)DOFsize);
+  out_torques_port.setDataSample(out_torques_var);
+  ports()->addPort(out_torques_port).doc("Output port for sending torque values");
+  const VecF zeros(DOFsize, 0.f);
+  for (RTT::OutputPort<VecF>* p :
+       {&out_jointPosLimitInf_port, &out_jointPosLimitSup_port, &out_jointVelLimitInf_port,
+        &out_jointVelLimitSup_port, &out_jointAccLimitInf_port, &out_jointAccLimitSup_port,
+        &out_jointAccDynLimitInf_port, &out_jointAccDynLimitSup_port, &out_jointTorqueLimitInf_port,
+        &out_jointTorqueLimitSup_port}) {
+    p->setDataSample(zeros);
+    ports()->addPort(*p).doc("Output port to give insight in robot's limit computed values");
+  }
+  portsPrepared_ = true;
+}
+
+void MotionGenerationQuadraticProgram::setGains(float kp, float kd) { ctl_.setGains(kp, kd); }
+
+static std::vector<double> as_double(const VecF& v) { return std::vector<double>(v.begin(), v.end()); }
+
+bool MotionGenerationQuadraticProgram::setTorqueLimits(std::vector<double> P, std::vector<double> N) {
+  return setTorqueLimitsE(VecF(P.begin(), P.end()), VecF(N.begin(), N.end()));
+}
+bool MotionGenerationQuadraticProgram::setAccelerationLimits(std::vector<double> P, std::vector<double> N) {
+  return setAccelerationLimitsE(VecF(P.begin(), P.end()), VecF(N.begin(), N.end()));
+}
+bool MotionGenerationQuadraticProgram::setAngularLimits(std::vector<double> S, std::vector<double> I) {
+  return setAngularLimitsE(VecF(S.begin(), S.end()), VecF(I.begin(), I.end()));
+}
+// the double -> float conversion happens here (doubleVToEigenV, src/mgqp.cpp:484-491); the
+// controller then stores the same float values
+bool MotionGenerationQuadraticProgram::setTorqueLimitsE(VecF P, VecF N) {
+  if (!ctl_.setTorqueLimits(as_double(P), as_double(N))) return false;
+  torquesP_ = P;
+  torquesN_ = N;
+  return true;
+}
+bool MotionGenerationQuadraticProgram::setAccelerationLimitsE(VecF P, VecF N) {
+  if (!ctl_.setAccelerationLimits(as_double(P), as_double(N))) return false;
+  accP_ = P;
+  accN_ = N;
+  return true;
+}
+bool MotionGenerationQuadraticProgram::setAngularLimitsE(VecF S, VecF I) {
+  return ctl_.setAngularLimits(as_double(S), as_double(I));
+}
+bool MotionGenerationQuadraticProgram::setPriorityLevel(std::string task, int level) {
+  return ctl_.setPriorityLevel(task, level);
+}
+
+// src/mgqp.cpp:142-170.  The reference falls off the end of this bool function after its
+// success message (undefined behaviour that in practice reports success); here it returns true.
+bool MotionGenerationQuadraticProgram::configureHook() {
+  if (!in_robotstatus_port.connected()) {
+    std::cout << "in_robotstatus_port not connected" << std::endl;
+    return false;
+  }
+  if (!in_h_port.connected()) {
+    std::cout << "in_h_port not connected" << std::endl;
+    return false;
+  }
+  if (!out_torques_port.connected()) {
+    std::cout << "out_torques_port not connected" << std::endl;
+    return false;
+  }
+  std::cout << "Controller configured SUCCESS !" << std::endl;
+  return true;
+}
+
+bool MotionGenerationQuadraticProgram::startHook() { return true; }
+
+// src/mgqp.cpp:872-1189.  Every port is read once per cycle into CycleInputs (Port::has is
+// "flow != RTT::NoData"; OldData carries the last sample, as RTT's read copies it), then the
+// controller's updateHook builds the stack, solves the hierarchy on the GPU and the outputs are
+// written.  Exceptions from the solver leave updateHook (RTT puts the component in Exception).
+// The reference's experiment timer (getSimulationTime() > 71 s -> stopHook, :1178-1188) is a
+// property of that Gazebo experiment and is not modelled.
+void MotionGenerationQuadraticProgram::updateHook() {
+  const RTT::FlowStatus rs = in_robotstatus_port.read(in_robotstatus_var);
+  const RTT::FlowStatus hf = in_h_port.read(in_h_var);
+  const RTT::FlowStatus mf = in_inertia_port.read(in_inertia_var);
+  if (hf == RTT::NoData || mf == RTT::NoData || rs == RTT::NoData) {
+    std::cout << "FAILED, NO DATA, RETURN" << std::endl;
+    last_code_ = CYCLE_NO_DATA;
+    return;
+  }
+  CycleInputs in;
+  in.robotstatus.set(JointState{in_robotstatus_var.angles, in_robotstatus_var.velocities});
+  in.h.set(in_h_var);
+  in.inertia.set(in_inertia_var);
+  in.joints.resize(DOFsize_);
+  auto rd = [](auto* port, auto& dst) {
+    typename std::remove_reference<decltype(dst.v)>::type v{};
+    if (port->read(v) != RTT::NoData) dst.set(v);
+  };
+  for (unsigned j = 0; j < DOFsize_; ++j) {
+    JointPorts& jp = in.joints[j];
+    rd(in_desiredTaskSpacePosition_port[j], jp.desiredTaskSpacePosition);
+    rd(in_desiredTaskSpaceVelocity_port[j], jp.desiredTaskSpaceVelocity);
+    rd(in_desiredTaskSpaceAcceleration_port[j], jp.desiredTaskSpaceAcceleration);
+    rd(in_desiredJointSpacePosition_port[j], jp.desiredJointSpacePosition);
+    rd(in_desiredJointSpaceVelocity_port[j], jp.desiredJointSpaceVelocity);
+    rd(in_desiredJointSpaceAcceleration_port[j], jp.desiredJointSpaceAcceleration);
+    rd(in_currentTaskSpacePosition_port[j], jp.currentTaskSpacePosition);
+    rd(in_currentTaskSpaceVelocity_port[j], jp.currentTaskSpaceVelocity);
+    rd(in_currentTaskSpaceAcceleration_port[j], jp.currentTaskSpaceAcceleration);
+    rd(in_jacobian_port[j], jp.jacobian);
+    rd(in_jacobianDot_port[j], jp.jacobianDot);
+  }
+  CycleOutputs out;
+  ctl_.updateHook(in, out);
+  last_code_ = out.code;
+  if (out.code != CYCLE_WRITTEN) {
+    std::cout << out.error << std::endl;
+    return;
+  }
+  out_torques_var.torques = out.torques;
+  out_jointPosLimitInf_port.write(out.jointPosLimitInf);
+  out_jointPosLimitSup_port.write(out.jointPosLimitSup);
+  out_jointVelLimitInf_port.write(out.jointVelLimitInf);
+  out_jointVelLimitSup_port.write(out.jointVelLimitSup);
+  out_jointAccLimitInf_port.write(out.jointAccLimitInf);
+  out_jointAccLimitSup_port.write(out.jointAccLimitSup);
+  out_jointAccDynLimitInf_port.write(out.jointAccDynLimitInf);
+  out_jointAccDynLimitSup_port.write(out.jointAccDynLimitSup);
+  out_jointTorqueLimitInf_port.write(out.jointTorqueLimitInf);
+  out_jointTorqueLimitSup_port.write(out.jointTorqueLimitSup);
+  out_torques_port.write(out_torques_var);
+}
+
+void MotionGenerationQuadraticProgram::stopHook() {  // src/mgqp.cpp:1191-1198
+  std::cout << "######################################\n"
+               "##                                  ##\n"
+               "##       END OF THE EXPERIMENT      ##\n"
+               "##                                  ##\n"
+               "######################################"
+            << std::endl;
+}
+
+void MotionGenerationQuadraticProgram::cleanupHook() {}
+
+// src/mgqp.cpp:1215-1267
+void MotionGenerationQuadraticProgram::printCurrentState() {
+  std::cout << "############## MotionGenerationQuadraticProgram State begin " << std::endl << std::endl;
+  const char* names[] = {"in_desiredTaskSpacePosition", "in_desiredTaskSpaceVelocity",
+                         "in_desiredTaskSpaceAcceleration", "in_desiredJointSpacePosition",
+                         "in_desiredJointSpaceVelocity", "in_desiredJointSpaceAcceleration"};
+  for (int i = 1; i <= (int)DOFsize_; ++i)
+    for (int j = 0; j < 6; ++j) {
+      const RTT::base::PortInterface* p =
+          j < 3 ? static_cast<RTT::base::PortInterface*>(
+                      (j == 0 ? in_desiredTaskSpacePosition_port
+                              : j == 1 ? in_desiredTaskSpaceVelocity_port : in_desiredTaskSpaceAcceleration_port)[i - 1])
+                : static_cast<RTT::base::PortInterface*>(
+                      (j == 3 ? in_desiredJointSpacePosition_port
+                              : j == 4 ? in_desiredJointSpaceVelocity_port : in_desiredJointSpaceAcceleration_port)[i - 1]);
+      if (!p->connected()) continue;
+      std::cout << names[j] << "_port_" << i << " connected -- ";
+      const int lvl = ctl_.stack_of_tasks.getLevel(std::string(names[j]) + "_" + std::to_string(i));
+      if (lvl != -1)
+        std::cout << " with priority " << lvl;
+      else
+        std::cout << " no priority // not considered ";
+      std::cout << std::endl;
+    }
+  std::cout << std::endl << std::endl;
+  std::cout << " degrees of freedom " << DOFsize_ << std::endl;
+  std::cout << " torque limits+ " << torquesP_ << std::endl;
+  std::cout << " torque limits- " << torquesN_ << std::endl;
+  std::cout << " acceleration limits+ " << accP_ << std::endl;
+  std::cout << " acceleration limits- " << accN_ << std::endl;
+  std::cout << " feedback angles " << in_robotstatus_var.angles << std::endl;
+  std::cout << " feedback velocities " << in_robotstatus_var.velocities << std::endl;
+  std::cout << " feedback torques " << in_robotstatus_var.torques << std::endl;
+  std::cout << " command torques " << out_torques_var.torques << std::endl;
+  std::cout << "############## MotionGenerationQuadraticProgram State end " << std::endl;
+}
+
+// src/mgqp.cpp:1270
+ORO_CREATE_COMPONENT_LIBRARY()
+ORO_LIST_COMPONENT_TYPE(MotionGenerationQuadraticProgram)
+
+}  // namespace rtt
+}  // namespace mgqp_amd
