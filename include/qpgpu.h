@@ -87,7 +87,9 @@ enum qpgpu_error {
                                           in batched use: it is extra HBM traffic. */
 
 #define QPGPU_FLAG_EXACT 0x2u         /* keep the reference's floating-point operation order
-                                          everywhere, so x and f are bit-identical to QuadProg++.
+                                          everywhere, so x and f are bit-identical to the CPU
+                                          restatement of QuadProg++'s order (SURVEY §3.2;
+                                          reference-pinned on the demo KAT only).
                                           Shapes up to n = 64 always do; for n > 64 the default
                                           runs the O(n^3) setup (Cholesky, J = L^-T, x0) as
                                           blocked f64 MFMA (qp_panel.hip), which matches the

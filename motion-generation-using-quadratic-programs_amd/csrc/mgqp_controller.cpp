@@ -764,7 +764,14 @@ void MotionGenerationQuadraticProgram::update_batched(const CycleInputs* in, Cyc
       o.error = e.what();
     }
   });
-  stack_of_tasks = count ? rob[count - 1].sot : stack_of_tasks;
+  // the member stack (what solveNextHierarchy() reads) is the last robot's that completed its
+  // cycle; a robot whose build or solve threw may hold a half-built stack, so it never leaks
+  // into the controller, and with no completed robot the member is left untouched
+  for (long r = count - 1; r >= 0; --r)
+    if (out[r].code == CYCLE_WRITTEN) {
+      stack_of_tasks = rob[r].sot;
+      break;
+    }
 }
 
 }  // namespace mgqp_amd

@@ -540,6 +540,8 @@ struct CycleWs {
   void* buf = nullptr;
   int64_t qp_count = -1;  // G / g0 initialised for this (count, dim)
   int qp_dim = -1;
+  int lim_m = -1, lim_n = -1;  // the constant limits matrix [-I; +I] uploaded for this (m, n)
+  size_t lim_off = 0;          // ... at this workspace offset
 };
 std::mutex g_cws_mu;
 std::map<std::pair<int, hipStream_t>, CycleWs> g_cws_map;
@@ -585,6 +587,7 @@ int run_cycle(const Plan& P, int64_t K, const float* Bcumul_host, float* torques
     g_cws.buf = nullptr;
     g_cws.bytes = 0;
     g_cws.qp_count = -1;
+    g_cws.lim_m = g_cws.lim_n = -1;
     if ((e = hipMalloc(&g_cws.buf, off)) != hipSuccess) return fail("hipMalloc", e, err);
     g_cws.bytes = off;
   }
@@ -607,9 +610,18 @@ int run_cycle(const Plan& P, int64_t K, const float* Bcumul_host, float* torques
          *x2 = reinterpret_cast<double*>(b + ox2), *f2 = reinterpret_cast<double*>(b + of2);
   int32_t *s1 = reinterpret_cast<int32_t*>(b + os1), *s2 = reinterpret_cast<int32_t*>(b + os2);
 
-  if ((e = hipMemcpyAsync(const_cast<float*>(W.Bcumul), Bcumul_host, (size_t)m * n * 4,
-                          hipMemcpyHostToDevice, s)) != hipSuccess)
-    return fail("hipMemcpyAsync", e, err);
+  // The limits matrix depends on the DOF only: uploaded once per (m, n) into the workspace, with
+  // a synchronous copy after the stream has drained (earlier cycles may still read the old one),
+  // so the caller's host buffer is never read after this call returns.
+  if (g_cws.lim_m != m || g_cws.lim_n != n || g_cws.lim_off != oB) {
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail("hipStreamSynchronize", e, err);
+    if ((e = hipMemcpy(const_cast<float*>(W.Bcumul), Bcumul_host, (size_t)m * n * 4,
+                       hipMemcpyHostToDevice)) != hipSuccess)
+      return fail("hipMemcpy", e, err);
+    g_cws.lim_m = m;
+    g_cws.lim_n = n;
+    g_cws.lim_off = oB;
+  }
   const bool init_qp = !(g_cws.qp_count == K && g_cws.qp_dim == n);
   if (launch_init(P, W, init_qp ? G : nullptr, g0, s)) return fail("init", hipGetLastError(), err);
   g_cws.qp_count = K;

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -230,6 +231,43 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
   return QPGPU_SUCCESS;
 }
 
+// Does the forced kernel family (if any) cover the shape?  Checked before any copy is queued.
+static bool family_covers(uint32_t flags, int n, int p, int m) {
+  if (flags & QPGPU_FLAG_FORCE_LANE) return qpk_lane_name(n, p, m) != nullptr;
+  if (flags & QPGPU_FLAG_FORCE_SUBGROUP) return qpk_small_name(n, p, m) != nullptr;
+  if (flags & QPGPU_FLAG_FORCE_WAVE) return qpk_medium_name(n, p, m) != nullptr;
+  return qpgpu_kernel_name(n, p, m)[0] != 0;
+}
+
+// Host-pointer entry (the drop-in's path, one QP per solve_quadprog() call, and the batched
+// controller's).  Device buffers are one allocation per thread, laid out
+//   [G | g0 | CE | ce0 | CI | ci0 | x || f | status | iters]
+// (256-B aligned pieces).  Batches up to kStagedBytes go through a pinned host staging buffer of
+// the same layout: the inputs are packed on the host, then ONE H2D copy, the launch and ONE D2H
+// copy of [x | f | status | iters] (+ G with WRITE_FACTOR) — instead of 7 + 4 pageable copies —
+// which is what a 50 ms control cycle's single solves need (latency, tools/dropin_latency.cpp).
+// Larger batches copy each array directly (a host-side pack would only add a pass over them).
+// QPGPU_HOST_STAGING=0 forces the direct copies (A/B measurement).
+static constexpr size_t kStagedBytes = 4u << 20;
+
+struct PinnedStage {
+  void* buf = nullptr;
+  size_t bytes = 0;
+  ~PinnedStage() {
+    if (buf) (void)hipHostFree(buf);
+  }
+};
+thread_local PinnedStage g_pin;
+
+static bool staging_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("QPGPU_HOST_STAGING");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const double* g0,
                              const double* CE, const double* ce0, const double* CI,
                              const double* ci0, double* x, double* f, int32_t* status,
@@ -240,7 +278,7 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const doubl
   if (!G || !g0 || !x || !f || !status) return QPGPU_ERR_INVALID_ARGUMENT;
   if ((d->p > 0 && (!CE || !ce0)) || (d->m > 0 && (!CI || !ci0)))
     return QPGPU_ERR_INVALID_ARGUMENT;
-  if (!qpgpu_kernel_name(d->n, d->p, d->m)[0]) return QPGPU_ERR_UNSUPPORTED_SHAPE;
+  if (!family_covers(d->flags, d->n, d->p, d->m)) return QPGPU_ERR_UNSUPPORTED_SHAPE;
   if (qpgpu_device_count() <= 0) {
     g_last_error = "no HIP device visible";
     return QPGPU_ERR_NO_DEVICE;
@@ -249,10 +287,13 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const doubl
   // per-QP-block arrays hold whole tiles in the TILED64 layout
   const size_t BB = d->layout == QPGPU_LAYOUT_TILED64 ? (B + 63) / 64 * 64 : B;
   auto al = [](size_t bytes) { return (bytes + 255) & ~(size_t)255; };
-  const size_t bG = al(BB * n * n * 8), bg0 = al(BB * n * 8), bCE = al(BB * n * p * 8),
-               bce0 = al(BB * p * 8), bCI = al(BB * n * m * 8), bci0 = al(BB * m * 8),
-               bx = al(BB * n * 8), bf = al(B * 8), bs = al(B * 4), bi = al(B * 4);
-  const size_t total = bG + bg0 + bCE + bce0 + bCI + bci0 + bx + bf + bs + bi;
+  const size_t nG = BB * n * n * 8, ng0 = BB * n * 8, nCE = BB * n * p * 8, nce0 = BB * p * 8,
+               nCI = BB * n * m * 8, nci0 = BB * m * 8, nx = BB * n * 8, nf = B * 8, ns = B * 4,
+               ni = B * 4;
+  // byte offsets of the pieces
+  const size_t oG = 0, og0 = oG + al(nG), oCE = og0 + al(ng0), oce0 = oCE + al(nCE),
+               oCI = oce0 + al(nce0), oci0 = oCI + al(nCI), ox = oci0 + al(nci0), of = ox + al(nx),
+               os = of + al(nf), oi = os + al(ns), total = oi + al(ni);
   hipError_t e;
   int dev = 0;
   if ((e = hipGetDevice(&dev)) != hipSuccess) return hip_fail(e, "hipGetDevice");
@@ -273,41 +314,81 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const doubl
       return hip_fail(e, "hipStreamCreate");
   }
   char* base = static_cast<char*>(g_ws.buf);
-  double* dG = reinterpret_cast<double*>(base);
-  double* dg0 = reinterpret_cast<double*>(base + bG);
-  double* dCE = reinterpret_cast<double*>(base + bG + bg0);
-  double* dce0 = reinterpret_cast<double*>(base + bG + bg0 + bCE);
-  double* dCI = reinterpret_cast<double*>(base + bG + bg0 + bCE + bce0);
-  double* dci0 = reinterpret_cast<double*>(base + bG + bg0 + bCE + bce0 + bCI);
-  double* dx = reinterpret_cast<double*>(base + bG + bg0 + bCE + bce0 + bCI + bci0);
-  double* df = reinterpret_cast<double*>(base + bG + bg0 + bCE + bce0 + bCI + bci0 + bx);
-  int32_t* dst =
-      reinterpret_cast<int32_t*>(base + bG + bg0 + bCE + bce0 + bCI + bci0 + bx + bf);
-  int32_t* dit =
-      reinterpret_cast<int32_t*>(base + bG + bg0 + bCE + bce0 + bCI + bci0 + bx + bf + bs);
+  auto D = [&](size_t off) { return reinterpret_cast<double*>(base + off); };
+  double* dG = D(oG);
   hipStream_t s = g_ws.stream;
-  auto h2d = [&](void* dst_, const void* src, size_t bytes) -> hipError_t {
+  const bool wf = (d->flags & QPGPU_FLAG_WRITE_FACTOR) != 0;
+  const bool staged = staging_enabled() && total <= kStagedBytes;
+  // after a failure past the first queued copy, drain the stream before returning so no copy
+  // still reads or writes the caller's buffers
+  auto fail_drain = [&](hipError_t err, const char* what) {
+    (void)hipStreamSynchronize(s);
+    return hip_fail(err, what);
+  };
+  if (staged) {
+    if (g_pin.bytes < total) {
+      if (g_pin.buf) (void)hipHostFree(g_pin.buf);
+      g_pin.buf = nullptr;
+      g_pin.bytes = 0;
+      if ((e = hipHostMalloc(&g_pin.buf, total, hipHostMallocDefault)) != hipSuccess)
+        return hip_fail(e, "hipHostMalloc");
+      g_pin.bytes = total;
+    }
+    char* h = static_cast<char*>(g_pin.buf);
+    auto put = [&](size_t off, const void* src, size_t bytes) {
+      if (bytes) std::memcpy(h + off, src, bytes);
+    };
+    put(oG, G, nG);
+    put(og0, g0, ng0);
+    put(oCE, CE, nCE);
+    put(oce0, ce0, nce0);
+    put(oCI, CI, nCI);
+    put(oci0, ci0, nci0);
+    put(ox, x, nx);  // x passes through unchanged on NONPD
+    if ((e = hipMemcpyAsync(base, h, of, hipMemcpyHostToDevice, s)) != hipSuccess)
+      return fail_drain(e, "hipMemcpyAsync H2D");
+    rc = qpgpu_solve_batched(d, dG, D(og0), D(oCE), D(oce0), D(oCI), D(oci0), D(ox), D(of),
+                             reinterpret_cast<int32_t*>(base + os),
+                             reinterpret_cast<int32_t*>(base + oi), s);
+    if (rc) {
+      (void)hipStreamSynchronize(s);
+      return rc;
+    }
+    if ((e = hipMemcpyAsync(h + ox, base + ox, total - ox, hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return fail_drain(e, "hipMemcpyAsync D2H");
+    if (wf && (e = hipMemcpyAsync(h + oG, base + oG, nG, hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return fail_drain(e, "hipMemcpyAsync D2H");
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    std::memcpy(x, h + ox, nx);
+    std::memcpy(f, h + of, nf);
+    std::memcpy(status, h + os, ns);
+    if (iters) std::memcpy(iters, h + oi, ni);
+    if (wf) std::memcpy(G, h + oG, nG);
+    return QPGPU_SUCCESS;
+  }
+  auto h2d = [&](size_t off, const void* src, size_t bytes) -> hipError_t {
     if (!bytes) return hipSuccess;
-    return hipMemcpyAsync(dst_, src, bytes, hipMemcpyHostToDevice, s);
+    return hipMemcpyAsync(base + off, src, bytes, hipMemcpyHostToDevice, s);
   };
-  if ((e = h2d(dG, G, BB * n * n * 8)) != hipSuccess || (e = h2d(dg0, g0, BB * n * 8)) != hipSuccess ||
-      (e = h2d(dCE, CE, BB * n * p * 8)) != hipSuccess ||
-      (e = h2d(dce0, ce0, BB * p * 8)) != hipSuccess ||
-      (e = h2d(dCI, CI, BB * n * m * 8)) != hipSuccess ||
-      (e = h2d(dci0, ci0, BB * m * 8)) != hipSuccess ||
-      (e = h2d(dx, x, BB * n * 8)) != hipSuccess)  // x passes through unchanged on NONPD
-    return hip_fail(e, "hipMemcpyAsync H2D");
-  rc = qpgpu_solve_batched(d, dG, dg0, dCE, dce0, dCI, dci0, dx, df, dst, dit, s);
-  if (rc) return rc;
-  auto d2h = [&](void* dst_, const void* src, size_t bytes) -> hipError_t {
-    return hipMemcpyAsync(dst_, src, bytes, hipMemcpyDeviceToHost, s);
+  if ((e = h2d(oG, G, nG)) != hipSuccess || (e = h2d(og0, g0, ng0)) != hipSuccess ||
+      (e = h2d(oCE, CE, nCE)) != hipSuccess || (e = h2d(oce0, ce0, nce0)) != hipSuccess ||
+      (e = h2d(oCI, CI, nCI)) != hipSuccess || (e = h2d(oci0, ci0, nci0)) != hipSuccess ||
+      (e = h2d(ox, x, nx)) != hipSuccess)  // x passes through unchanged on NONPD
+    return fail_drain(e, "hipMemcpyAsync H2D");
+  rc = qpgpu_solve_batched(d, dG, D(og0), D(oCE), D(oce0), D(oCI), D(oci0), D(ox), D(of),
+                           reinterpret_cast<int32_t*>(base + os),
+                           reinterpret_cast<int32_t*>(base + oi), s);
+  if (rc) {
+    (void)hipStreamSynchronize(s);
+    return rc;
+  }
+  auto d2h = [&](void* dst_, size_t off, size_t bytes) -> hipError_t {
+    return hipMemcpyAsync(dst_, base + off, bytes, hipMemcpyDeviceToHost, s);
   };
-  if ((d->flags & QPGPU_FLAG_WRITE_FACTOR) && (e = d2h(G, dG, BB * n * n * 8)) != hipSuccess)
-    return hip_fail(e, "hipMemcpyAsync D2H");
-  if ((e = d2h(x, dx, BB * n * 8)) != hipSuccess || (e = d2h(f, df, B * 8)) != hipSuccess ||
-      (e = d2h(status, dst, B * 4)) != hipSuccess ||
-      (iters && (e = d2h(iters, dit, B * 4)) != hipSuccess))
-    return hip_fail(e, "hipMemcpyAsync D2H");
+  if (wf && (e = d2h(G, oG, nG)) != hipSuccess) return fail_drain(e, "hipMemcpyAsync D2H");
+  if ((e = d2h(x, ox, nx)) != hipSuccess || (e = d2h(f, of, nf)) != hipSuccess ||
+      (e = d2h(status, os, ns)) != hipSuccess || (iters && (e = d2h(iters, oi, ni)) != hipSuccess))
+    return fail_drain(e, "hipMemcpyAsync D2H");
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
   return QPGPU_SUCCESS;
 }

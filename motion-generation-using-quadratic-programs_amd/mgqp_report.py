@@ -85,17 +85,18 @@ def write_reports(path: str, rows, dof: int = 7, ws: int = 3) -> None:
 def read_reports(path: str, dof: int = 7, ws: int = 3) -> dict:
     """plotresult.m's parse (collapse spaces, skip the header line, numeric matrix), returned
     as {column name: series} plus the matrix under "data"."""
+    names = columns(dof, ws)
     rows = []
     with open(path) as f:
-        next(f)
-        for line in f:
+        next(f, None)  # header (an empty file has none)
+        for lineno, line in enumerate(f, start=2):
             parts = line.split()
-            if parts:
-                rows.append([float(v) for v in parts])
-    data = np.asarray(rows, np.float64).reshape(len(rows), -1)
-    names = columns(dof, ws)
-    if data.shape[1] != len(names):
-        raise ValueError(f"{path}: {data.shape[1]} columns, expected {len(names)}")
+            if not parts:
+                continue
+            if len(parts) != len(names):
+                raise ValueError(f"{path}:{lineno}: {len(parts)} columns, expected {len(names)}")
+            rows.append([float(v) for v in parts])
+    data = np.asarray(rows, np.float64).reshape(len(rows), len(names))
     out = {n: data[:, i] for i, n in enumerate(names)}
     out["data"] = data
     return out

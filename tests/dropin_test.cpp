@@ -4,7 +4,9 @@
 // Built by __graft_entry__.build(); run by tests/test_gpu_dropin.py on the GPU box.
 #include <cmath>
 #include <cstdio>
+#include <cstdint>
 #include <cstring>
+#include <vector>
 #include <limits>
 #include <stdexcept>
 #include <string>
@@ -22,7 +24,52 @@ static int fails = 0;
 
 static bool same_bits(double a, double b) { return std::memcmp(&a, &b, 8) == 0; }
 
-int main() {
+// --qp FILE: solve every QP of a binary batch (int32 count, n, p, m; then per QP G n*n, g0 n,
+// CE n*p (the t(CE) layout), ce0 p, CI n*m, ci0 m — doubles) one solve_quadprog() call at a time,
+// the way mgqp calls it (constraint ROWS, then ArrayHH::t() temporaries), and print per QP
+// "f <hex> x <hex...> G <hex...>" or the exception.  tests/test_gpu_dropin.py compares the lines
+// with the oracle, bit for bit.
+static int solve_file(const char* path) {
+  FILE* fp = std::fopen(path, "rb");
+  if (!fp) return 2;
+  int32_t hdr[4];
+  if (std::fread(hdr, 4, 4, fp) != 4) return 2;
+  const int cnt = hdr[0], n = hdr[1], p = hdr[2], m = hdr[3];
+  std::vector<double> buf((size_t)n * n + n + n * p + p + n * m + m);
+  for (int q = 0; q < cnt; ++q) {
+    if (std::fread(buf.data(), 8, buf.size(), fp) != buf.size()) return 2;
+    const double* v = buf.data();
+    Matrix<double> G(n, n), CEr(p, n), CIr(m, n);
+    Vector<double> g0(n), ce0(p), ci0(m), x;
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) G[i][j] = *v++;
+    for (int i = 0; i < n; ++i) g0[i] = *v++;
+    for (int i = 0; i < n; ++i)
+      for (int k = 0; k < p; ++k) CEr[k][i] = *v++;
+    for (int k = 0; k < p; ++k) ce0[k] = *v++;
+    for (int i = 0; i < n; ++i)
+      for (int k = 0; k < m; ++k) CIr[k][i] = *v++;
+    for (int k = 0; k < m; ++k) ci0[k] = *v++;
+    try {
+      const double f = solve_quadprog(G, g0, ArrayHH::t(CEr), ce0, ArrayHH::t(CIr), ci0, x);
+      std::printf("f %a x", f);
+      for (int i = 0; i < n; ++i) std::printf(" %a", x[i]);
+      std::printf(" G");
+      for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) std::printf(" %a", G[i][j]);
+      std::printf("\n");
+    } catch (const std::runtime_error& e) {
+      std::printf("runtime_error %s\n", e.what());
+    } catch (const std::logic_error& e) {
+      std::printf("logic_error %s\n", e.what());
+    }
+  }
+  std::fclose(fp);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 2 && std::string(argv[1]) == "--qp") return solve_file(argv[2]);
   // 1. QuadProg++ demo (SURVEY §4 archive output: f = 12, x = [1, 2.0000000000000009])
   {
     Matrix<double> G(2, 2), CE(2, 1), CI(2, 3);
@@ -136,6 +183,34 @@ int main() {
       what = e.what();
     }
     CHECK(what == "The matrix CE is incompatible (incorrect number of rows 3 , expecting 2)");
+  }
+  // 5. shapes no kernel covers: the documented exceptions (include/quadprog_amd/QuadProg++.hh)
+  {
+    Matrix<double> G(0, 0), CE(0, 0), CI(0, 0);
+    Vector<double> g0(0), ce0(0), ci0(0), x;
+    std::string what;
+    try {
+      solve_quadprog(G, g0, CE, ce0, CI, ci0, x);
+    } catch (const std::logic_error& e) {
+      what = e.what();
+    }
+    CHECK(what == "qpgpu: n == 0 is not supported (undefined in QuadProg++)");
+  }
+  {
+    const unsigned n = 300;  // above qpgpu_max_n()
+    Matrix<double> G(n, n), CE(n, 0), CI(n, 0);
+    Vector<double> g0(n), ce0(0), ci0(0), x;
+    for (unsigned i = 0; i < n; i++) {
+      g0[i] = 1.0;
+      for (unsigned j = 0; j < n; j++) G[i][j] = (i == j) ? 1.0 : 0.0;
+    }
+    std::string what;
+    try {
+      solve_quadprog(G, g0, CE, ce0, CI, ci0, x);
+    } catch (const std::runtime_error& e) {
+      what = e.what();
+    }
+    CHECK(what == "qpgpu: solve failed (code 2): no gfx950 kernel covers this (n, p, m)");
   }
   std::printf("dropin_test: %s (%d failures)\n", fails ? "FAIL" : "OK", fails);
   return fails ? 1 : 0;

@@ -1,12 +1,14 @@
 // eigen_api_test.cpp — exercises the Eigen-variant drop-in (include/quadprog_amd/eigen/
 // QuadProg++.hh: QuadProgpp::Solver::solve -> Status, reference eigen/QuadProg++.hh:83-118)
-// against the ArrayHH drop-in solve_quadprog (libquadprog_amd.so) on the same problems.
+// against the ArrayHH drop-in solve_quadprog (libquadprog_amd.so) on the same problems, and
+// (--qp mode, tests/test_gpu_dropin.py) against the CPU oracle.
 // Eigen is not installed here, so the Eigen code path is exercised through an Eigen-like
 // column-major matrix type (rows()/cols()/operator()(i, j)) instantiating the same template the
 // Eigen signature calls; the ArrayHH build of the header (QUADPROGPP_DISABLE_EIGEN) is the
 // Solver itself.  Built by __graft_entry__.build(); run by tests/test_gpu_dropin.py.
 #include <cmath>
 #include <cstdio>
+#include <cstdint>
 #include <cstring>
 #include <limits>
 #include <stdexcept>
@@ -94,7 +96,51 @@ static Prob make(unsigned n, unsigned p, unsigned m, unsigned seed, bool infeasi
   return P;
 }
 
-int main() {
+// --qp FILE (same batch format as dropin_test --qp): every QP through QuadProgpp::Solver
+// (QuadProgpp containers) and through the column-major generic path; prints per QP
+// "A <status> <f hex> <x hex...>" and "C <status> <f hex> <x hex...>" (status: QPGPU_QP_*).
+// tests/test_gpu_dropin.py compares both with the oracle, bit for bit.
+static int solve_file(const char* path) {
+  FILE* fp = std::fopen(path, "rb");
+  if (!fp) return 2;
+  int32_t hdr[4];
+  if (std::fread(hdr, 4, 4, fp) != 4) return 2;
+  const unsigned cnt = hdr[0], n = hdr[1], p = hdr[2], m = hdr[3];
+  std::vector<double> buf((size_t)n * n + n + n * p + p + n * m + m);
+  QuadProgpp::Solver qp;
+  for (unsigned q = 0; q < cnt; ++q) {
+    if (std::fread(buf.data(), 8, buf.size(), fp) != buf.size()) return 2;
+    const double* v = buf.data();
+    QuadProgpp::Matrix<double> Gs(n, n), CEs(n, p), CIs(n, m);
+    QuadProgpp::Vector<double> g0s(n), ce0s(p), ci0s(m), xs;
+    ColMat Gc(n, n), CEc(n, p), CIc(n, m);
+    ColVec g0c(n), ce0c(p), ci0c(m), xc;
+    for (unsigned i = 0; i < n; ++i)
+      for (unsigned j = 0; j < n; ++j) Gs[i][j] = Gc(i, j) = *v++;
+    for (unsigned i = 0; i < n; ++i) g0s[i] = g0c[i] = *v++;
+    for (unsigned i = 0; i < n; ++i)
+      for (unsigned k = 0; k < p; ++k) CEs[i][k] = CEc(i, k) = *v++;
+    for (unsigned k = 0; k < p; ++k) ce0s[k] = ce0c[k] = *v++;
+    for (unsigned i = 0; i < n; ++i)
+      for (unsigned k = 0; k < m; ++k) CIs[i][k] = CIc(i, k) = *v++;
+    for (unsigned k = 0; k < m; ++k) ci0s[k] = ci0c[k] = *v++;
+    qp.solve(Gs, g0s, CEs, ce0s, CIs, ci0s, xs);
+    std::printf("A %d %a", qp.detailed_status(), qp.objective());
+    for (unsigned i = 0; i < n; ++i) std::printf(" %a", xs[i]);
+    std::printf("\n");
+    QuadProgpp::amd_detail::Staging stg;
+    double fc = 0.0;
+    const int stc = QuadProgpp::amd_detail::solve_generic(stg, Gc, g0c, CEc, ce0c, CIc, ci0c, xc, fc);
+    std::printf("C %d %a", stc, fc);
+    for (unsigned i = 0; i < n; ++i) std::printf(" %a", xc[i]);
+    std::printf("\n");
+  }
+  std::fclose(fp);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 2 && std::string(argv[1]) == "--qp") return solve_file(argv[2]);
   // 1. QuadProg++ demo through the Solver (ArrayHH containers): same bits as solve_quadprog;
   //    G is left unchanged (the fork factors a copy)
   {

@@ -338,6 +338,31 @@ int main(int argc, char** argv) {
     CHECK(r2.torques.read(none) == RTT::NoData);
   }
 
+  // update_batched: the controller's member stack comes from the last robot that completed its
+  // cycle, never from a robot whose solve threw (here the last one: dependent equalities)
+  {
+    mgqp_amd::MotionGenerationQuadraticProgram bc;
+    configure_direct(bc, sup, inf, dof);
+    std::vector<mgqp_amd::CycleInputs> ins;
+    ins.push_back(as_inputs(make_cycle(dof, sup, inf), dof));
+    mgqp_amd::CycleInputs bad = as_inputs(make_cycle(dof, sup, inf), dof);
+    MatF J(3, dof, 0.f);
+    for (int r = 0; r < 3; ++r) J(r, 0) = 1.f;  // three identical task rows on level 0
+    bad.joints[dof - 1].jacobian.set(J);
+    ins.push_back(bad);
+    std::vector<mgqp_amd::CycleOutputs> outs(2);
+    bc.update_batched(ins.data(), outs.data(), 2, 1);
+    CHECK(outs[0].code == mgqp_amd::CYCLE_WRITTEN && outs[1].code == mgqp_amd::CYCLE_EXCEPTION);
+    mgqp_amd::MotionGenerationQuadraticProgram one;
+    configure_direct(one, sup, inf, dof);
+    mgqp_amd::CycleOutputs o1;
+    one.updateHook(ins[0], o1);
+    const auto& a = bc.stack_of_tasks.qps[0];
+    const auto& b = one.stack_of_tasks.qps[0];
+    CHECK(a.conditions.rows == b.conditions.rows && a.conditions.a == b.conditions.a &&
+          a.goal == b.goal && a.limits == b.limits);
+  }
+
   std::printf("%s: %d cycles through ports == CycleInputs path (bitwise), %d failures\n",
               g_fail ? "FAILED" : "OK", written, g_fail);
   return g_fail ? 1 : 0;

@@ -70,3 +70,16 @@ def test_rows_from_controller_cycles(gpu, tmp_path):
     rep.write_reports(path, rows)
     back = rep.read_reports(path)
     assert np.array_equal(back["data"][:, 41:48], np.asarray(torques, np.float64))
+
+
+def test_read_reports_header_only_and_ragged(tmp_path):
+    import mgqp_report as mr
+
+    p = tmp_path / "reports.dat"
+    p.write_text("# " + " ".join(mr.columns(7, 3)) + "\n")
+    r = mr.read_reports(str(p))
+    assert r["data"].shape == (0, len(mr.columns(7, 3)))
+    n = len(mr.columns(7, 3))
+    p.write_text("# h\n" + " ".join(["1"] * n) + "\n" + " ".join(["1"] * (n - 1)) + "\n")
+    with pytest.raises(ValueError, match=r"reports.dat:3: .* columns, expected"):
+        mr.read_reports(str(p))
