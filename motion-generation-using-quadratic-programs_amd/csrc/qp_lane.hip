@@ -85,14 +85,21 @@ constexpr int kScanDepth = QPGPU_SCAN_DEPTH;
 #ifndef QPGPU_LANE_CI_LDS
 #define QPGPU_LANE_CI_LDS 1
 #endif
-// warm the caches with this lane's CI / ci0 lines before the equality phase (QP-major layout).
-// Off by default: measured (profiles/r01_s2/lane_ci_warmup.log) it shortens the mean wave (scan
-// 36k -> 28k cycles) but lowers the pipelined throughput ~4 % on C1 and C2 — the extra
-// uncoalesced loads compete with other launches' scans.
+// warm the caches with this lane's CI / ci0 lines before the equality phase (QP-major layout):
+// 0 never, 1 always, 2 when p > 0 (an equality phase long enough for the loads to land).
+// Measured on cold inputs (profiles/r02_s2/bench_C{1,2}_{base,pf}.log): C1 (p = 6) kernel
+// 55.4 -> 52.6 us and +3 % pipelined; C2 (p = 0, no equality phase) 78.1 -> 80.5 us.  Round 1
+// measured it on one warm input set (lane_ci_warmup.log), where it lost ~4 % pipelined.
 #ifndef QPGPU_LANE_PREFETCH
-#define QPGPU_LANE_PREFETCH 0
+#define QPGPU_LANE_PREFETCH 2
 #endif
-constexpr bool kLanePrefetch = QPGPU_LANE_PREFETCH != 0;
+// keep the CI rows that do not fit the LDS (and ci0) in registers from the first l1 scan on, so
+// later scans issue no global loads (EXACT QP-major shapes with the LDS rows only): 0 never,
+// 1 always, 2 when p > 0 (the p = 0 loop holds J and the Givens state in registers already: with
+// the rows too it spills to scratch)
+#ifndef QPGPU_LANE_CI_REGS
+#define QPGPU_LANE_CI_REGS 0
+#endif
 static_assert(kScanDepth >= 2, "the pipelined scan needs at least two row buffers");
 
 __device__ __forceinline__ bool wave_any(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
@@ -104,6 +111,7 @@ template <int NM, int MM, int T, bool EXACT, int QPW, int PX>
 __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const QpArgs a) {
   constexpr bool kJregLoopCfg = QPGPU_LANE_JREG_LOOP == 2 || (QPGPU_LANE_JREG_LOOP == 1 && PX == 0);
   constexpr bool kRbRegs = QPGPU_LANE_RB_REGS == 2 || (QPGPU_LANE_RB_REGS == 1 && PX != 0);
+  constexpr bool kLanePrefetch = QPGPU_LANE_PREFETCH == 1 || (QPGPU_LANE_PREFETCH == 2 && PX > 0);
   static_assert(QPW == 64 || (QPW == 32 && T == 1), "half waves only with the QP-major layout");
   static_assert(MM <= 64, "bitmask bookkeeping holds m <= 64");
   using RI = RIdx<NM>;
@@ -382,7 +390,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
       return Jr_(i, j);
   };
   const auto kReg = std::true_type{};
-  const auto kLds = std::false_type{};
+  [[maybe_unused]] const auto kLds = std::false_type{};
   auto compute_d = [&](auto InReg) {
 #pragma unroll
     for (int c = 0; c < NM; c++) {
@@ -632,6 +640,10 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   // rows from LDS — no extra global traffic and nothing to wait for.
   const bool ci_lds = QPGPU_LANE_CI_LDS && kCiRows > 0 && (a.flags & kArgAligned16);
   bool ci_ready = false;  // wave-uniform: the LDS copy has been written
+  // rows kCiRows..NM-1 of CI and ci0 (index NM - kCiRows) in registers (QPGPU_LANE_CI_REGS)
+  constexpr bool kCiRegs = (QPGPU_LANE_CI_REGS == 1 || (QPGPU_LANE_CI_REGS == 2 && PX > 0)) && kCiRows > 0;
+  constexpr int kRegRows = kCiRegs ? NM + 1 - kCiRows : 1;
+  [[maybe_unused]] double cireg[kRegRows][MM];
   // element e (= row * MM + column) of this lane's CI from the LDS copy (e < kCiRows * MM)
   auto ci_lds_at = [&](int e) -> double { return sbuf[((e >> 1) * QPW + lane) * 2 + (e & 1)]; };
   qp_stamp(a, 2);
@@ -741,6 +753,11 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
           const bool from_lds = ci_lds && ci_ready;
           const bool fill_lds = ci_lds && !ci_ready;
           auto load_row = [&](int r, double* dst) {
+            if (kCiRegs && from_lds && r >= kCiRows && r <= NM) {
+#pragma unroll
+              for (int i = 0; i < MM; i++) dst[i] = cireg[r - kCiRows < kRegRows ? r - kCiRows : 0][i];
+              return;
+            }
             if (r < NM) {
               if (r < kCiRows && from_lds) {
 #pragma unroll
@@ -782,8 +799,16 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
                   *reinterpret_cast<double2*>(sbuf + (((j * MM + i) >> 1) * QPW + lane) * 2) =
                       double2{rowbuf[j % D][i], rowbuf[j % D][i + 1]};
               }
+              if (kCiRegs && j >= kCiRows && fill_lds) {
+#pragma unroll
+                for (int i = 0; i < MM; i++) cireg[j - kCiRows < kRegRows ? j - kCiRows : 0][i] = rowbuf[j % D][i];
+              }
             }
             __builtin_amdgcn_sched_barrier(0);
+          }
+          if (kCiRegs && fill_lds) {
+#pragma unroll
+            for (int i = 0; i < MM; i++) cireg[kRegRows - 1][i] = rowbuf[NM % D][i];
           }
 #pragma unroll
           for (int i = 0; i < MM; i++)

@@ -57,6 +57,22 @@ for s in $STEPS; do
     benchcold)
       for c in C1 C2 mgqp C3; do run benchcold_$c 600 python bench.py --config $c --no-cpu --steps 20; done
       run benchcold_C5 600 python bench.py --config C5 --no-cpu --steps 3 --warmup 1 --kernel-reps 3 ;;
+    latency)
+      run latency 300 tools/dropin_latency 2000 500
+      QPGPU_HOST_STAGING=0 run latency_nostage 300 tools/dropin_latency 2000 500 ;;
+    ab)
+      # A/B of the in-tree build against _ab/<variant>/libqpgpu.so (tools/ab_build.sh), per config
+      for c in ${CONFIGS:-C1 C2}; do
+        run bench_${c}_base 600 python bench.py --config $c --no-cpu --steps 30
+        for v in ${VARIANTS}; do
+          QPGPU_LIB_PATH=_ab/$v/libqpgpu.so run bench_${c}_$v 600 python bench.py --config $c --no-cpu --steps 30
+        done
+      done ;;
+    abpar)
+      # parity of an A/B variant: the full-size C1/C2 and edge-case parity tests against it
+      for v in ${VARIANTS}; do
+        QPGPU_LIB_PATH=_ab/$v/libqpgpu.so run parity_$v 600 python -m pytest tests/test_gpu_parity.py -m gpu -q -x -k "full_size or edge or config_parity or batch_tail or c4_shard"
+      done ;;
     listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;
     sq)
       for f in ${FAMILIES:-lane subgroup}; do
