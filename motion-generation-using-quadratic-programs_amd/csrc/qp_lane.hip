@@ -100,6 +100,26 @@ constexpr int kScanDepth = QPGPU_SCAN_DEPTH;
 #ifndef QPGPU_LANE_CI_REGS
 #define QPGPU_LANE_CI_REGS 0
 #endif
+// add_constraint's Givens sweep: feed distance() the carried |h| of the previous rotation (or
+// the untouched d[j]) instead of the rotated d[j] = +-h, so the chain of h values does not wait
+// for the cc = d/h division and sign select (distance() reads magnitudes only: same bits).
+// Measured neutral on C1 (equality phase 26.4k cycles/wave either way, profiles/r02_s4): off.
+#ifndef QPGPU_LANE_HCHAIN
+#define QPGPU_LANE_HCHAIN 0
+#endif
+// issue the CI / ci0 cache warm-up right after the G / CE staging instead of after the setup.
+// Measured slower (C1 kernel 54.0 -> 56.5 us, setup 21.7k -> 33.4k cycles/wave: vmcnt waits are
+// in issue order, so the G / CE waits then cover the warm-up loads too): off.
+#ifndef QPGPU_LANE_PF_EARLY
+#define QPGPU_LANE_PF_EARLY 0
+#endif
+// l1 scans after the first (CI rows 0..kCiRows-1 in LDS): issue every global row (the rest of
+// CI and ci0) at the start of the scan, then sum the LDS rows while they are in flight.
+// Measured (profiles/r02_s4): C1 kernel 54.0 -> 51.7 us on cold inputs, scan 18.9k -> 16.6k
+// cycles/wave, bitwise parity unchanged.
+#ifndef QPGPU_LANE_SCANG
+#define QPGPU_LANE_SCANG 1
+#endif
 static_assert(kScanDepth >= 2, "the pipelined scan needs at least two row buffers");
 
 __device__ __forceinline__ bool wave_any(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
@@ -202,6 +222,25 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   // one dword per 128-B line of this lane's CI / ci0 blocks (cache warm-up, see below)
   constexpr int kPfCI = (NM * MM * 8 + 127) / 128 + 1, kPfC0 = (MM * 8 + 127) / 128 + 1;
   [[maybe_unused]] uint32_t pf[kPfCI + kPfC0];
+  // Touch every cache line of this lane's CI and ci0 blocks before the equality phase: the
+  // loads complete during it (nothing waits on them until its end), so the first l1 scan — all
+  // lanes of every wave at about the same time — reads L2 / MALL instead of queueing on one
+  // chip-wide HBM burst.
+  auto warmup = [&]() {
+  if constexpr (T == 1 && kLanePrefetch) {
+    if (live) {
+      const char* c = reinterpret_cast<const char*>(a.CI + b * (int64_t)(n * m));
+      const char* c0 = reinterpret_cast<const char*>(a.ci0 + b * (int64_t)m);
+      const int bc = n * m * 8, b0c = m * 8;
+#pragma unroll
+      for (int k = 0; k < kPfCI; k++)
+        pf[k] = (bc >= 4) ? *reinterpret_cast<const uint32_t*>(c + min(k * 128, bc - 4)) : 0u;
+#pragma unroll
+      for (int k = 0; k < kPfC0; k++)
+        pf[kPfCI + k] = (b0c >= 4) ? *reinterpret_cast<const uint32_t*>(c0 + min(k * 128, b0c - 4)) : 0u;
+    }
+  }
+  };
   qp_stamp(a, 0);
 
   // ---------------------------------------------------------------- setup
@@ -231,6 +270,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
         stage_all(a.ce0, p, offc);
       }
     }
+    if constexpr (QPGPU_LANE_PF_EARLY) warmup();
 #pragma unroll
     for (int i = 0; i < NM; i++)
       if (i < n) c1 += Gr[i][i];
@@ -343,23 +383,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
     }
   }
   qp_stamp(a, 1);
-  // Touch every cache line of this lane's CI and ci0 blocks before the equality phase: the
-  // loads complete during it (nothing waits on them until its end), so the first l1 scan — all
-  // lanes of every wave at about the same time — reads L2 / MALL instead of queueing on one
-  // chip-wide HBM burst.
-  if constexpr (T == 1 && kLanePrefetch) {
-    if (live) {
-      const char* c = reinterpret_cast<const char*>(a.CI + b * (int64_t)(n * m));
-      const char* c0 = reinterpret_cast<const char*>(a.ci0 + b * (int64_t)m);
-      const int bc = n * m * 8, b0c = m * 8;
-#pragma unroll
-      for (int k = 0; k < kPfCI; k++)
-        pf[k] = (bc >= 4) ? *reinterpret_cast<const uint32_t*>(c + min(k * 128, bc - 4)) : 0u;
-#pragma unroll
-      for (int k = 0; k < kPfC0; k++)
-        pf[kPfCI + k] = (b0c >= 4) ? *reinterpret_cast<const uint32_t*>(c0 + min(k * 128, b0c - 4)) : 0u;
-    }
-  }
+  if constexpr (!QPGPU_LANE_PF_EARLY) warmup();
   if (!chol_ok) {
     status = QPGPU_QP_NOT_POSITIVE_DEFINITE;
     fval = bad_sum;
@@ -433,11 +457,14 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   auto add_constraint = [&](auto InReg, auto LoC) -> bool {
     constexpr int LO = decltype(LoC)::value;
     if (iq >= n) return false;  // reference UB (p > n); reported as dependent
+    // |d[j]| as the rotation at j sees it: the previous rotation's h (applied) or the original
+    double carried = 0.0;
 #pragma unroll
     for (int j = NM - 1; j >= LO + 1; j--) {
       if (j <= n - 1 && j >= iq + 1) {
         double cc = dv[j - 1], ss = dv[j];
-        const double h = qp_distance(cc, ss);
+        const double h = qp_distance(cc, (QPGPU_LANE_HCHAIN && j < n - 1) ? carried : ss);
+        carried = (fabs(h) < kEps) ? cc : h;
         if (!(fabs(h) < kEps)) {
           dv[j] = 0.0;
           ss = ss / h;
@@ -782,6 +809,39 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
                 for (int i = 0; i < MM; i++) dst[i] = (i < m) ? ldci0(i) : 0.0;
             }
           };
+          if (QPGPU_LANE_SCANG && kCiRows > 0 && !kCiRegs && from_lds) {
+            // every global row in flight first, the LDS rows summed meanwhile (same j order)
+            constexpr int NG = NM + 1 - (kCiRows > 0 ? kCiRows : 0);
+            double gbuf[NG][MM];
+#pragma unroll
+            for (int r = NM + 1 - NG; r <= NM; r++) load_row(r, gbuf[r - (NM + 1 - NG)]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < NM; j++) {
+              if (j < n) {
+                const double xj = xv[j];
+                if (j < NM + 1 - NG) {
+#pragma unroll
+                  for (int i = 0; i < MM; i += 2) {
+                    const double2 v =
+                        *reinterpret_cast<const double2*>(sbuf + (((j * MM + i) >> 1) * QPW + lane) * 2);
+                    if (i < m) sv[i] += v.x * xj;
+                    if (i + 1 < m) sv[i + 1] += v.y * xj;
+                  }
+                } else {
+#pragma unroll
+                  for (int i = 0; i < MM; i++)
+                    if (i < m) sv[i] += gbuf[j - (NM + 1 - NG) < NG ? j - (NM + 1 - NG) : 0][i] * xj;
+                }
+              }
+            }
+#pragma unroll
+            for (int i = 0; i < MM; i++)
+              if (i < m) {
+                sv[i] += gbuf[NG - 1][i];
+                psi += (sv[i] < 0.0) ? sv[i] : 0.0;
+              }
+          } else {
 #pragma unroll
           for (int r = 0; r < D - 1; r++) load_row(r, rowbuf[r % D]);
 #pragma unroll
@@ -816,6 +876,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
               sv[i] += rowbuf[NM % D][i];
               psi += (sv[i] < 0.0) ? sv[i] : 0.0;
             }
+          }
         }
         ci_ready = ci_lds;
         if (do_scan) {

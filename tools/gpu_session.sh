@@ -73,6 +73,10 @@ for s in $STEPS; do
       for v in ${VARIANTS}; do
         QPGPU_LIB_PATH=_ab/$v/libqpgpu.so run parity_$v 600 python -m pytest tests/test_gpu_parity.py -m gpu -q -x -k "full_size or edge or config_parity or batch_tail or c4_shard"
       done ;;
+    abstamps)
+      # per-phase stamps (tools/stamps.py) of the in-tree build and each A/B variant
+      run stamps_base 300 python tools/stamps.py ${KIND:-general}
+      for v in ${VARIANTS}; do QPGPU_LIB_PATH=_ab/$v/libqpgpu.so run stamps_$v 300 python tools/stamps.py ${KIND:-general}; done ;;
     listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;
     sq)
       for f in ${FAMILIES:-lane subgroup}; do
