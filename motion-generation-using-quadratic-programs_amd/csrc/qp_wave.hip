@@ -135,6 +135,32 @@ __device__ __forceinline__ double seq_fms_down(double s, int k0, int k1, FA A, F
   return s;
 }
 
+// Value of v held by lane i of this thread's subgroup (S = 32: lanes i and 32 + i of the wave
+// serve the two QPs; S = 64: lane i).  i must be wave-uniform (a compile-time step index): two
+// or four v_readlane per double, no LDS round trip.
+template <int S>
+__device__ __forceinline__ double sg_bcast(double v, int i) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+  const uint32_t l0 = __builtin_amdgcn_readlane(lo, i), h0 = __builtin_amdgcn_readlane(hi, i);
+  if constexpr (S == 64) {
+    return __builtin_bit_cast(double, ((uint64_t)h0 << 32) | l0);
+  } else {
+    static_assert(S == 32, "sg_bcast: one or two QPs per wave");
+    const uint32_t l1 = __builtin_amdgcn_readlane(lo, 32 + i), h1 = __builtin_amdgcn_readlane(hi, 32 + i);
+    const bool up = threadIdx.x >= 32;
+    return __builtin_bit_cast(double, ((uint64_t)(up ? h1 : h0) << 32) | (up ? l1 : l0));
+  }
+}
+
+// Register-resident setup for the one-wave variants (S <= 64, LDS J/R, launched at one wave per
+// SIMD so registers are plentiful): lane j keeps row j of G/L (Cholesky), lane r builds row r of
+// J = L^{-T} by column-oriented forward substitution, and cholesky_solve runs across the lanes
+// with v_readlane broadcasts.  Every element sees the reference's operations in the reference's
+// order (see the block), so results are bitwise unchanged.
+#ifndef QPGPU_WAVE_REGSETUP
+#define QPGPU_WAVE_REGSETUP 1
+#endif
 // per-QP control block (lead lane writes, subgroup reads after grp_sync)
 struct Ctl {
   double f, t, t1, t2, ss, R_norm, c1, c2, psi, ci0ip, znp;
@@ -184,6 +210,7 @@ template <int S, int NMAX, int MMAX, bool GJR, int OCC = 1>
 __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
     qp_wave_kernel(const QpArgs a, double* __restrict__ ws) {
   using C = WaveCfg<S, NMAX, MMAX, GJR>;
+  constexpr bool kRegSetup = QPGPU_WAVE_REGSETUP && !GJR && S == 32 && NMAX <= 32 && OCC == 1;
   // loads in flight per lane in the global-operand sums (deeper for the one-QP-per-workgroup
   // workspace variant, whose lanes have registers to spare)
   constexpr int KG = GJR ? 16 : kUG;
@@ -274,36 +301,93 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
     ctl->fin = 1;
   }
   grp_sync<S>();
-  if (live && !pre) {
-    if (lead) {
-      double c1 = 0.0;
-      for (int i = 0; i < n; i++) c1 += R_(i, i);
-      ctl->c1 = c1;
-    }
-    // cholesky_decomposition (@.text+0x2df0): row-wise, descending-k sums, upper mirrored.
-    for (int i = 0; i < n; i++) {
+  if constexpr (kRegSetup) {
+    // cholesky_decomposition (@.text+0x2df0) with lane j holding row j of G / L in registers.
+    // Step i: sum = A[i][j] - sum_{k=i-1..0} L[i][k] L[j][k] (k descending) on every lane
+    // j >= i (lane i: the pivot sum with A[i][i]); L[i][i-1] comes from lane i by v_readlane,
+    // the older L[i][k] and the upper G[i][j] from LDS; the pivot is broadcast, every lane takes
+    // the same sqrt, and lanes j > i divide.  Column i is published lower and mirrored upper at
+    // once, as the reference leaves it after row i.  The inner loops are branch-free (row
+    // indices clamped; lanes and entries past n compute values nobody reads) so their loads
+    // issue together.
+    if (live) {
       if (lead) {
-        const double sum = seq_fms_down<GJR ? kUG : kUL>(R_(i, i), 0, i, [&](int k) { return R_(i, k); },
-                                        [&](int k) { return R_(i, k); });
-        if (sum <= 0.0) {
-          ctl->status = QPGPU_QP_NOT_POSITIVE_DEFINITE;
-          ctl->f = sum;
-        } else {
-          ctl->t = sqrt(sum);  // the pivot, shared with the subgroup
+        double c1 = 0.0;
+        for (int i = 0; i < n; i++) c1 += R_(i, i);
+        ctl->c1 = c1;
+      }
+      const int j = ls;
+      const bool mine = j < n;
+      const int jc = mine ? j : n - 1;
+      double A[NMAX];
+#pragma unroll
+      for (int k = 0; k < NMAX; k++) A[k] = R_(jc, k < n ? k : n - 1);
+      bool fail = false;
+      double bad = 0.0;
+#pragma unroll
+      for (int i = 0; i < NMAX; i++) {
+        if (i < n && !fail) {
+          const double lnew = i > 0 ? sg_bcast<S>(A[i > 0 ? i - 1 : 0], i) : 0.0;  // L[i][i-1]
+          double lold[NMAX];
+#pragma unroll
+          for (int k = 0; k + 1 < i; k++) lold[k] = R_(i, k);
+          double sum = (j == i) ? A[i] : R_(i, jc);
+#pragma unroll
+          for (int k = i - 1; k >= 0; k--) sum -= ((k == i - 1) ? lnew : lold[k]) * A[k];
+          const double sd = sg_bcast<S>(sum, i);
+          if (sd <= 0.0) {
+            fail = true;
+            bad = sd;
+          } else {
+            const double dg = sqrt(sd);
+            const double v = (j == i) ? dg : sum / dg;
+            if (mine && j >= i) {
+              A[i] = v;
+              R_(j, i) = v;
+              if (j > i) R_(i, j) = v;
+            }
+          }
+          sg_sync();
         }
       }
-      grp_sync<S>();
-      if (ctl->status != QPGPU_QP_OK) break;
-      const double dg = ctl->t;
-      for (int j = i + 1 + ls; j < n; j += S) {
-        const double s2 = seq_fms_down<GJR ? kUG : kUL>(R_(i, j), 0, i, [&](int k) { return R_(i, k); },
-                                       [&](int k) { return R_(j, k); });
-        R_(j, i) = s2 / dg;
+      if (lead && fail) {
+        ctl->status = QPGPU_QP_NOT_POSITIVE_DEFINITE;
+        ctl->f = bad;
       }
-      if (lead) R_(i, i) = dg;
-      grp_sync<S>();
-      for (int k = i + 1 + ls; k < n; k += S) R_(i, k) = R_(k, i);
-      grp_sync<S>();
+    }
+    grp_sync<S>();
+  } else {
+    if (live && !pre) {
+      if (lead) {
+        double c1 = 0.0;
+        for (int i = 0; i < n; i++) c1 += R_(i, i);
+        ctl->c1 = c1;
+      }
+      // cholesky_decomposition (@.text+0x2df0): row-wise, descending-k sums, upper mirrored.
+      for (int i = 0; i < n; i++) {
+        if (lead) {
+          const double sum = seq_fms_down<GJR ? kUG : kUL>(R_(i, i), 0, i, [&](int k) { return R_(i, k); },
+                                          [&](int k) { return R_(i, k); });
+          if (sum <= 0.0) {
+            ctl->status = QPGPU_QP_NOT_POSITIVE_DEFINITE;
+            ctl->f = sum;
+          } else {
+            ctl->t = sqrt(sum);  // the pivot, shared with the subgroup
+          }
+        }
+        grp_sync<S>();
+        if (ctl->status != QPGPU_QP_OK) break;
+        const double dg = ctl->t;
+        for (int j = i + 1 + ls; j < n; j += S) {
+          const double s2 = seq_fms_down<GJR ? kUG : kUL>(R_(i, j), 0, i, [&](int k) { return R_(i, k); },
+                                         [&](int k) { return R_(j, k); });
+          R_(j, i) = s2 / dg;
+        }
+        if (lead) R_(i, i) = dg;
+        grp_sync<S>();
+        for (int k = i + 1 + ls; k < n; k += S) R_(i, k) = R_(k, i);
+        grp_sync<S>();
+      }
     }
   }
   qp_stamp(a, 1);
@@ -312,57 +396,131 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
     double* Gw = a.G + qbase_rt(bb, n * n, T);
     for (int e = ls; e < n * n; e += S) EL(Gw, e) = R_(e / n, e - (e / n) * n);
   }
-  if (chol_ok && !pre) {
-    // J = L^{-T}: lane r builds row r = (L^{-1} e_r)^T in place (J_(r, .) is its own scratch).
-    // With a finite L the first r entries are exactly +0.0 and add exact zeros later: skipped
-    // (same bits).  A non-finite L takes the literal path.
-    if (lead) {
-      int fin = 1;
-      for (int i = 0; i < n && fin; i++)
-        for (int j = 0; j <= i; j++)
-          if (!(fabs(R_(i, j)) < inf)) {
-            fin = 0;
-            break;
-          }
-      ctl->fin = fin;
+  if constexpr (kRegSetup) {
+    if (chol_ok) {
+      const int j = ls;
+      const bool mine = j < n;
+      const int jc = mine ? j : n - 1;
+      // J = L^{-T}: lane r builds row r = (L^{-1} e_r)^T by column-oriented forward
+      // substitution: at step q, y_q = s_q / L[q][q], then s_i -= L[i][q] y_q for i > q — for
+      // each i the same subtractions in the same (q ascending) order as the reference's row
+      // sums.  The reference's literal form throughout (for a finite L its first r entries are
+      // +0.0 and subtract exact zeros: the skip of the LDS path changes no bits).  Column q of L
+      // is row q of the mirrored upper triangle (contiguous: paired broadcast reads).  The
+      // running sums sit in a window that shifts one entry per step (w[k] = s_{q+k}), so the
+      // step loop stays rolled with compile-time register indices; entries past n are never
+      // stored.
+      double w[NMAX];
+#pragma unroll
+      for (int k = 0; k < NMAX; k++) w[k] = (k == j) ? 1.0 : 0.0;
+      for (int q = 0; q < n; q++) {
+        const double* Lq = Rm + q * JS + q;  // Lq[k] = L[q+k][q] (k >= 1), Lq[0] = L[q][q]
+        double lc[NMAX];
+#pragma unroll
+        for (int k = 0; k < NMAX; k++) lc[k] = Lq[k];
+        const double y = w[0] / lc[0];
+        if (mine) J_(j, q) = y;
+#pragma unroll
+        for (int k = 0; k + 1 < NMAX; k++) w[k] = w[k + 1] - lc[k + 1] * y;
+        w[NMAX - 1] = 0.0;
+      }
+      // cholesky_solve (@.text+0x31a2) across the lanes: forward y = L^{-1} g0 column-oriented
+      // (lane i accumulates its row's subtractions in q order), backward x = L^{-T} y row by row
+      // (lane k forms U[k][i] x_i as soon as x_i is broadcast; lane i subtracts them in i+1..n-1
+      // order, the reference's; entries past n stay +0.0 and subtract nothing).  Row j of the
+      // factor array holds both L[j][q] (q < j) and U[j][i] (i > j).  Divisors broadcast with
+      // v_readlane.
+      const double diag = R_(jc, jc);
+      double yv = zv[jc];
+      for (int q = 0; q < n; q++) {
+        const double lq = R_(jc, q);
+        const double yq = sg_bcast<S>(yv / diag, q);
+        const double upd = yv - lq * yq;
+        yv = (j == q) ? yq : ((j > q) ? upd : yv);
+      }
+      double Lr[NMAX];
+#pragma unroll
+      for (int k = 0; k < NMAX; k++) Lr[k] = R_(jc, k);
+      double P[NMAX];
+#pragma unroll
+      for (int k = 0; k < NMAX; k++) P[k] = 0.0;
+      double xm = 0.0;
+#pragma unroll
+      for (int i = NMAX - 1; i >= 0; i--) {
+        double v = yv;
+#pragma unroll
+        for (int k = i + 1; k < NMAX; k++) v -= P[k];
+        const double xi = sg_bcast<S>(v / diag, i);
+        xm = (j == i) ? xi : xm;
+        P[i] = (j < i && i < n) ? Lr[i] * xi : 0.0;
+      }
+      if (mine) xv[j] = -xm;
+      grp_sync<S>();
+      if (lead) {
+        double c2 = 0.0;
+        for (int i = 0; i < n; i++) c2 += J_(i, i);
+        ctl->c2 = c2;
+        double f = 0.0;
+        for (int i = 0; i < n; i++) f += zv[i] * xv[i];
+        ctl->f = 0.5 * f;
+        ctl->R_norm = 1.0;
+        ctl->iq = 0;
+      }
+      grp_sync<S>();
     }
-    grp_sync<S>();
-    const bool skip = ctl->fin != 0;
-    for (int r = ls; r < n; r += S) {
-      const int i0 = skip ? r : 0;
-      for (int i = 0; i < i0; i++) J_(r, i) = 0.0;
-      for (int i = i0; i < n; i++) {
-        const double v = seq_fms_up<GJR ? kUG : kUL>((i == r) ? 1.0 : 0.0, i0, i, [&](int j) { return R_(i, j); },
-                                    [&](int j) { return J_(r, j); });
-        J_(r, i) = v / R_(i, i);
+  } else {
+    if (chol_ok && !pre) {
+      // J = L^{-T}: lane r builds row r = (L^{-1} e_r)^T in place (J_(r, .) is its own scratch).
+      // With a finite L the first r entries are exactly +0.0 and add exact zeros later: skipped
+      // (same bits).  A non-finite L takes the literal path.
+      if (lead) {
+        int fin = 1;
+        for (int i = 0; i < n && fin; i++)
+          for (int j = 0; j <= i; j++)
+            if (!(fabs(R_(i, j)) < inf)) {
+              fin = 0;
+              break;
+            }
+        ctl->fin = fin;
       }
+      grp_sync<S>();
+      const bool skip = ctl->fin != 0;
+      for (int r = ls; r < n; r += S) {
+        const int i0 = skip ? r : 0;
+        for (int i = 0; i < i0; i++) J_(r, i) = 0.0;
+        for (int i = i0; i < n; i++) {
+          const double v = seq_fms_up<GJR ? kUG : kUL>((i == r) ? 1.0 : 0.0, i0, i, [&](int j) { return R_(i, j); },
+                                      [&](int j) { return J_(r, j); });
+          J_(r, i) = v / R_(i, i);
+        }
+      }
+      grp_sync<S>();
+      if (lead) {
+        double c2 = 0.0;
+        for (int i = 0; i < n; i++) c2 += J_(i, i);
+        ctl->c2 = c2;
+        // cholesky_solve (@.text+0x31a2): y -> d, x = -G^{-1} g0
+        for (int i = 0; i < n; i++) {
+          const double v = seq_fms_up<GJR ? kUG : kUL>(zv[i], 0, i, [&](int j) { return R_(i, j); },
+                                      [&](int j) { return dv[j]; });
+          dv[i] = v / R_(i, i);
+        }
+        for (int i = n - 1; i >= 0; i--) {
+          const double v = seq_fms_up<GJR ? kUG : kUL>(dv[i], i + 1, n, [&](int j) { return R_(i, j); },
+                                      [&](int j) { return xv[j]; });
+          xv[i] = v / R_(i, i);
+        }
+        double f = 0.0;
+        for (int i = 0; i < n; i++) {
+          xv[i] = -xv[i];
+          f += zv[i] * xv[i];
+        }
+        ctl->f = 0.5 * f;
+        ctl->R_norm = 1.0;
+        ctl->iq = 0;
+      }
+      grp_sync<S>();
     }
-    grp_sync<S>();
-    if (lead) {
-      double c2 = 0.0;
-      for (int i = 0; i < n; i++) c2 += J_(i, i);
-      ctl->c2 = c2;
-      // cholesky_solve (@.text+0x31a2): y -> d, x = -G^{-1} g0
-      for (int i = 0; i < n; i++) {
-        const double v = seq_fms_up<GJR ? kUG : kUL>(zv[i], 0, i, [&](int j) { return R_(i, j); },
-                                    [&](int j) { return dv[j]; });
-        dv[i] = v / R_(i, i);
-      }
-      for (int i = n - 1; i >= 0; i--) {
-        const double v = seq_fms_up<GJR ? kUG : kUL>(dv[i], i + 1, n, [&](int j) { return R_(i, j); },
-                                    [&](int j) { return xv[j]; });
-        xv[i] = v / R_(i, i);
-      }
-      double f = 0.0;
-      for (int i = 0; i < n; i++) {
-        xv[i] = -xv[i];
-        f += zv[i] * xv[i];
-      }
-      ctl->f = 0.5 * f;
-      ctl->R_norm = 1.0;
-      ctl->iq = 0;
-    }
-    grp_sync<S>();
   }
   if (chol_ok) {
     // R = 0 (L no longer needed), flags

@@ -32,6 +32,18 @@ def _relerr(a, b):
     return float(np.max(r)) if r.size else 0.0
 
 
+def _bit_mismatch(a, b, show=6):
+    """Elements whose bits differ, as (gpu hex, oracle hex) pairs.  Two NaNs count as equal: IEEE
+    754 leaves the sign and payload of a NaN that an invalid operation creates (inf - inf, 0 * inf,
+    sqrt(-x)) to the implementation — x86 creates 0xfff8..., gfx950 0x7ff8... — so only the fact
+    that a value is NaN is part of the reference behaviour, not its bits."""
+    a = np.ascontiguousarray(a, dtype=np.float64).ravel()
+    b = np.ascontiguousarray(b, dtype=np.float64).ravel()
+    diff = (a.view(np.uint64) != b.view(np.uint64)) & ~(np.isnan(a) & np.isnan(b))
+    idx = np.where(diff)[0][:show]
+    return [(float(a[i]).hex(), float(b[i]).hex()) for i in idx]
+
+
 FAMILIES = (None, "lane", "subgroup", "wave")
 
 
@@ -66,11 +78,12 @@ def assert_parity(pr, label, max_iter=0, write_factor=False, family=None, layout
     assert ex <= TOL and ef <= TOL, f"{label}: rel err x {ex:.3e} f {ef:.3e}"
     if not bitwise_expected(pr.n, write_factor, exact):
         return so, io
-    bit_x = np.array_equal(xg[ok].view(np.uint64), xo[ok].view(np.uint64))
-    bit_f = np.array_equal(fg.view(np.uint64), fo.view(np.uint64))
-    assert bit_x and bit_f, f"{label}: within tolerance but not bitwise (x {ex:.3e}, f {ef:.3e})"
+    bx, bf = _bit_mismatch(xg[ok], xo[ok]), _bit_mismatch(fg, fo)
+    assert not bx and not bf, (f"{label}: within tolerance but not bitwise (x {ex:.3e}, f {ef:.3e}); "
+                               f"x (gpu, oracle) {bx}; f (gpu, oracle) {bf}")
     if write_factor:
-        assert np.array_equal(prg.G.view(np.uint64), prc.G.view(np.uint64)), f"{label}: factor differs"
+        bg = _bit_mismatch(prg.G, prc.G)
+        assert not bg, f"{label}: factor differs (gpu, oracle) {bg}"
     return so, io
 
 
@@ -121,6 +134,24 @@ def test_panel_setup_not_pd(gpu):
     pr.G[1, :, :] = np.eye(n)
     pr.G[1, 3, 3] = 0.0       # first block, fourth pivot
     assert_parity(pr, "panel not_pd")
+
+
+@pytest.mark.parametrize("layout", ["qp_major", "tiled64"])
+@pytest.mark.parametrize("write_factor", [False, True])
+@pytest.mark.parametrize("n,p,m,B", [(30, 6, 60, 65), (32, 8, 64, 64), (24, 0, 60, 33)])
+def test_wave_one_wave_per_simd_edges(gpu, n, p, m, B, write_factor, layout):
+    """The qp_wave variant launched at one wave per SIMD (LDS > 20 KiB per block: C3-sized QPs),
+    whose Cholesky / J / x0 run in registers across the lanes: failing pivots first, inside and
+    last, non-finite G entries (the reference's literal J path), the factor written back, and
+    an odd batch (the last wave's second QP is idle)."""
+    pr = qp_cases.make("general", n, p, m, B, seed=n + B)
+    pr.G[0, 5, 5] = -1.0e3      # fails at pivot 5
+    pr.G[1, 0, 0] = -1.0        # fails at pivot 0
+    pr.G[2, n - 1, n - 1] = 0.0  # fails (or nearly) at the last pivot
+    pr.G[3, 3, 7] = pr.G[3, 7, 3] = np.nan
+    pr.G[4, 2, 2] = np.inf
+    pr.G[5, 4, 9] = 1.0e300      # huge off-diagonal: overflow in the later pivots
+    assert_parity(pr, f"wave edges n={n}", write_factor=write_factor, family="wave", layout=layout)
 
 
 @pytest.mark.parametrize("family", FAMILIES)

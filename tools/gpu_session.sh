@@ -77,6 +77,12 @@ for s in $STEPS; do
       # per-phase stamps (tools/stamps.py) of the in-tree build and each A/B variant
       run stamps_base 300 python tools/stamps.py ${KIND:-general}
       for v in ${VARIANTS}; do QPGPU_LIB_PATH=_ab/$v/libqpgpu.so run stamps_$v 300 python tools/stamps.py ${KIND:-general}; done ;;
+    wavecheck)
+      # qp_wave changes: parity on every wave-covered shape, then C3 / mgqp-level benches and stamps
+      run wave_parity 900 python -m pytest tests/test_gpu_parity.py -m gpu -q -x -rf -k "wave or config_parity or large_config or panel or edge or tail"
+      run bench_C3 600 python bench.py --config C3 --no-cpu --steps 10 --warmup 3
+      run bench_mgqp 600 python bench.py --config mgqp --no-cpu --steps 20
+      run stamps_C3 300 python tools/stamps_wave.py 30 6 60 65536 ;;
     listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;
     sq)
       for f in ${FAMILIES:-lane subgroup}; do
