@@ -14,6 +14,8 @@
 // State lives in LDS (per QP: J and R [n][n+1], vectors, bookkeeping) with dynamic indexing;
 // with GJR, J and R live in a global workspace instead (n = 256: 2 x 514 KiB per QP).  The
 // lead lane exchanges scalars with its subgroup through an LDS control block.
+#include <climits>
+
 #include "qp_common.h"
 
 namespace qpk {
@@ -153,11 +155,42 @@ __device__ __forceinline__ double sg_bcast(double v, int i) {
   }
 }
 
+// Subgroup argmin for S <= 64 (xor butterfly): the smallest v, ties to the smallest index — the
+// result of a sequential `if (v < best)` scan in index order.  Lanes without a candidate pass
+// (+inf, INT_MAX); the caller never offers +inf as a candidate.
+template <int S>
+__device__ __forceinline__ void sg_argmin(double& v, int& i) {
+  static_assert(S <= 64, "one wave per subgroup");
+#pragma unroll
+  for (int o = 1; o < S; o <<= 1) {
+    const double v2 = __shfl_xor(v, o, S);
+    const int i2 = __shfl_xor(i, o, S);
+    const bool take = (v2 < v) || (v2 == v && i2 < i);
+    v = take ? v2 : v;
+    i = take ? i2 : i;
+  }
+}
+
 // Register-resident setup for the one-wave variants (S <= 64, LDS J/R, launched at one wave per
 // SIMD so registers are plentiful): lane j keeps row j of G/L (Cholesky), lane r builds row r of
 // J = L^{-T} by column-oriented forward substitution, and cholesky_solve runs across the lanes
 // with v_readlane broadcasts.  Every element sees the reference's operations in the reference's
 // order (see the block), so results are bitwise unchanged.
+// CI columns kept in registers across the active-set loop (one-wave-per-SIMD variant): measured
+// slower (C3 16.7 vs 15.4 ms, profiles/r02_s8: the 128 extra live VGPRs cost the loop's other
+// phases AGPR copies and scratch), so off; the scan instead issues all of a lane's CI loads at
+// once (kScanWide)
+// l1 scan with all of a lane's CI loads issued at once (buffer loads): measured slower (C3
+// 16.0 vs 15.3 ms, scan 196k vs 144k cycles per block, profiles/r02_s10): off
+#ifndef QPGPU_WAVE_FALLTHRU
+#define QPGPU_WAVE_FALLTHRU 1
+#endif
+#ifndef QPGPU_WAVE_SCANWIDE
+#define QPGPU_WAVE_SCANWIDE 0
+#endif
+#ifndef QPGPU_WAVE_CIREG
+#define QPGPU_WAVE_CIREG 0
+#endif
 #ifndef QPGPU_WAVE_REGSETUP
 #define QPGPU_WAVE_REGSETUP 1
 #endif
@@ -211,6 +244,15 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
     qp_wave_kernel(const QpArgs a, double* __restrict__ ws) {
   using C = WaveCfg<S, NMAX, MMAX, GJR>;
   constexpr bool kRegSetup = QPGPU_WAVE_REGSETUP && !GJR && S == 32 && NMAX <= 32 && OCC == 1;
+  // lane-parallel selections (argmin of s for l2, of u/r for t1) for one-wave subgroups
+  constexpr bool kLaneSel = S <= 64;
+  // the one-wave-per-SIMD variant keeps each lane's CI columns (and ci0) in registers from the
+  // first l1 scan on
+  constexpr bool kCiReg = QPGPU_WAVE_CIREG && kRegSetup && MMAX <= 64 && MMAX % S == 0;
+  constexpr int kCU = kCiReg ? MMAX / S : 1;
+  // l1 scan with every CI load of a lane in flight at once (<= 2 constraints per lane)
+  constexpr bool kScanWide = QPGPU_WAVE_SCANWIDE && !kCiReg && kRegSetup && MMAX <= 2 * S;
+  constexpr int kWU = (MMAX + S - 1) / S;
   // loads in flight per lane in the global-operand sums (deeper for the one-QP-per-workgroup
   // workspace variant, whose lanes have registers to spare)
   constexpr int KG = GJR ? 16 : kUG;
@@ -601,16 +643,26 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
   // the lead's two step dot products z.z and z.np, one pass (two independent chains)
   auto dot2_lead = [&](double& zz, double& znp) {
     double s1 = 0.0, s2 = 0.0;
-    for (int i = 0; i < n; i++) {
-      const double z = zv[i];
-      s1 += z * z;
-      s2 += z * npv[i];
+    constexpr int U = 8;  // loads of a chunk issued together (the adds stay in i order)
+    for (int ib = 0; ib < n; ib += U) {
+      double zc[U], pc[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        zc[u] = ib + u < n ? zv[ib + u] : 0.0;
+        pc[u] = ib + u < n ? npv[ib + u] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (ib + u < n) {
+          s1 += zc[u] * zc[u];
+          s2 += zc[u] * pc[u];
+        }
     }
     zz = s1;
     znp = s2;
   };
   auto dot_lead = [&](const double* u_, const double* v_) {
-    return seq_fma_up<kUL>(0.0, 0, n, [&](int i) { return u_[i]; }, [&](int i) { return v_[i]; });
+    return seq_fma_up<8>(0.0, 0, n, [&](int i) { return u_[i]; }, [&](int i) { return v_[i]; });
   };
   // add_constraint (@.text+0x21fd), split in three:
   //  1. the lead runs the serial part of the d-chain.  Rotation g (j = n-1-g) computes
@@ -630,14 +682,22 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
       int ng = 0;
       if (iq < n) {
         double carried = dv[n - 1];
-        for (int j = n - 1; j >= iq + 1; j--) {
-          const double a0 = dv[j - 1];
-          const double h = qp_distance(a0, carried);
-          const bool skip = fabs(h) < kEps;
-          gf[ng] = skip ? 0.0 : 1.0;
-          gx[ng] = h;
-          carried = skip ? a0 : h;
-          ng++;
+        constexpr int U = 8;  // d values of a chunk loaded together, ahead of the h chain
+        for (int jb = n - 1; jb >= iq + 1; jb -= U) {
+          double ac[U];
+#pragma unroll
+          for (int u = 0; u < U; u++) ac[u] = jb - u >= iq + 1 ? dv[jb - u - 1] : 0.0;
+#pragma unroll
+          for (int u = 0; u < U; u++)
+            if (jb - u >= iq + 1) {
+              const double a0 = ac[u];
+              const double h = qp_distance(a0, carried);
+              const bool skip = fabs(h) < kEps;
+              gf[ng] = skip ? 0.0 : 1.0;
+              gx[ng] = h;
+              carried = skip ? a0 : h;
+              ng++;
+            }
         }
       }
       ctl->ngiv = ng;
@@ -711,13 +771,14 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
       }
     }
     grp_sync<S>();
+    if (iq0 < n)  // R[:iq+1, iq] = d[:iq+1], one entry per lane
+      for (int i = ls; i <= iq0; i += S) R_(i, iq0) = dv[i];
     if (lead) {
       int iq = ctl->iq;
       if (iq >= n) {
         ctl->fin = 0;  // reference UB (p > n); reported as dependent
       } else {
         iq++;
-        for (int i = 0; i < iq; i++) R_(i, iq - 1) = dv[i];
         ctl->iq = iq;
         const double dd = fabs(dv[iq - 1]);
         if (dd <= kEps * ctl->R_norm) {
@@ -846,7 +907,6 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
         if (fabs(zz) > kEps) t2 = (-dot_lead(npv, xv) - EL(ce0b, i)) / znp;
         ctl->t2 = t2;
         uv[iq] = t2;
-        for (int k = 0; k < iq; k++) uv[k] -= t2 * rv[k];
         ctl->f += 0.5 * (t2 * t2) * znp;
         Av[i] = -i - 1;
       }
@@ -854,6 +914,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
       {
         const double t2 = ctl->t2;
         for (int k = ls; k < n; k += S) xv[k] += t2 * zv[k];
+        for (int k = ls; k < ctl->iq; k += S) uv[k] -= t2 * rv[k];
       }
       add_constraint();
       if (!ctl->fin) {
@@ -887,9 +948,14 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
   const int max_steps = a.max_steps;
   // diagnostic phase clocks (stamps only): scan, select, d/z, lead step, add, delete
   uint64_t tph[6] = {0, 0, 0, 0, 0, 0};
+  [[maybe_unused]] double cir[kCU][kCiReg ? NMAX : 1], c0r[kCU];
+  [[maybe_unused]] bool ci_in_regs = false;
   auto clk = [&]() -> uint64_t { return a.stamps ? __builtin_amdgcn_s_memtime() : 0; };
+  // A QP falls through scan -> select -> step within one pass of the loop (QPGPU_WAVE_FALLTHRU),
+  // so two QPs of a wave at different phases share the later blocks instead of running them in
+  // separate passes.
   while (true) {
-    const int phase = ctl->phase;
+    int phase = ctl->phase;
     if (S < 64) {
       if (__builtin_amdgcn_ballot_w64(phase != PH_DONE) == 0) break;
     } else if (phase == PH_DONE) {
@@ -899,50 +965,155 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
     if (phase == PH_SCAN) {
       const uint64_t t0 = clk();
       // ---- l1
-      if (lead) {
-        ctl->iter++;
-        for (int i = p; i < ctl->iq; i++) act[Av[i]] = 1;
+      if (lead) ctl->iter++;
+      {
+        // mark the active inequalities; keep the rollback copies of A and u (read only after a
+        // degenerate add_constraint, so they may be taken whether or not the scan finds ψ = 0)
+        const int iqs = ctl->iq;
+        for (int i = ls; i < iqs; i += S) {
+          const int ai = Av[i];
+          if (i >= p) act[ai] = 1;
+          Ao[i] = ai;
+          uo[i] = uv[i];
+        }
       }
-      for (int i = ls; i < m; i += S) {
-        const double c0 = EL(ci0b, i);  // issued with the first chunk, added last
-        double s = seq_fma_up<KG>(0.0, 0, n, [&](int j) { return EL(CIb, j * m + i); },
-                              [&](int j) { return xv[j]; });
-        s += c0;
-        sv[i] = s;
-        exc[i] = 0;
+      if constexpr (kCiReg) {
+        // columns ls + u*S of CI (and ci0) stay in registers after the first scan; entries past
+        // n are +0.0 against x = +0.0, and adding +0.0 leaves every partial sum unchanged (a
+        // running sum from +0.0 is never -0.0)
+        if (!ci_in_regs) {
+          const int64_t rs = (int64_t)m * T;  // element stride between CI rows
+#pragma unroll
+          for (int u = 0; u < kCU; u++) {
+            const int i = ls + u * S;
+            const double* cb = CIb + (int64_t)(i < m ? i : 0) * T;
+#pragma unroll
+            for (int j = 0; j < NMAX; j++) cir[u][j] = (i < m && j < n) ? cb[j * rs] : 0.0;
+            c0r[u] = i < m ? EL(ci0b, i) : 0.0;
+          }
+          ci_in_regs = true;
+        }
+#pragma unroll
+        for (int u = 0; u < kCU; u++) {
+          const int i = ls + u * S;
+          double s = 0.0;
+#pragma unroll
+          for (int j = 0; j < NMAX; j++) s += cir[u][j] * (j < n ? xv[j] : 0.0);
+          s += c0r[u];
+          if (i < m) {
+            sv[i] = s;
+            exc[i] = 0;
+          }
+        }
+      } else if constexpr (kScanWide) {
+        // all of this lane's CI column loads issued before the first multiply-add (one memory
+        // latency per scan); entries past n are +0.0 against x = +0.0 (no-op adds, see above)
+        // buffer loads off the wave's first QP (uniform descriptor): one offset VGPR per lane,
+        // the row stride in the scalar offset
+        const int64_t wb0 = (int64_t)blockIdx.x * C::QPB;
+        const double* ciw = a.CI + qbase_rt(wb0, n * m, T);
+        const uint64_t cp = reinterpret_cast<uint64_t>(ciw);
+        // readfirstlane returns int: keep both halves unsigned (no sign extension into the high
+        // word) so the descriptor's base is the pointer
+        const uint32_t cp_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cp);
+        const uint32_t cp_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cp >> 32));
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void*>(((uint64_t)cp_hi << 32) | cp_lo), 0, 0x7fffffff, 0x00020000);
+        const int qoff = live ? (int)(qbase_rt(bb, n * m, T) - qbase_rt(wb0, n * m, T)) : 0;
+        double cw[kWU][NMAX], c0w[kWU];
+#pragma unroll
+        for (int u = 0; u < kWU; u++) {
+          const int i = ls + u * S;
+          const int vo = (qoff + (i < m ? i : 0) * T) * 8;
+#pragma unroll
+          for (int j = 0; j < NMAX; j++)
+            cw[u][j] = (i < m && j < n)
+                           ? __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                            rsrc, vo, (j < n ? j : 0) * m * T * 8, 0))
+                           : 0.0;
+          c0w[u] = i < m ? EL(ci0b, i) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kWU; u++) {
+          const int i = ls + u * S;
+          double s = 0.0;
+#pragma unroll
+          for (int j = 0; j < NMAX; j++) s += cw[u][j] * (j < n ? xv[j] : 0.0);
+          s += c0w[u];
+          if (i < m) {
+            sv[i] = s;
+            exc[i] = 0;
+          }
+        }
+      } else {
+        for (int i = ls; i < m; i += S) {
+          const double c0 = EL(ci0b, i);  // issued with the first chunk, added last
+          double s = seq_fma_up<KG>(0.0, 0, n, [&](int j) { return EL(CIb, j * m + i); },
+                                [&](int j) { return xv[j]; });
+          s += c0;
+          sv[i] = s;
+          exc[i] = 0;
+        }
       }
       grp_sync<S>();
       if (lead) {
         double psi = 0.0;
-        for (int i = 0; i < m; i++) psi += (sv[i] < 0.0) ? sv[i] : 0.0;
+        constexpr int U = 8;  // loads of a chunk together, adds in i order
+        for (int ib = 0; ib < m; ib += U) {
+          double sc[U];
+#pragma unroll
+          for (int u = 0; u < U; u++) sc[u] = ib + u < m ? sv[ib + u] : 0.0;
+#pragma unroll
+          for (int u = 0; u < U; u++)
+            if (ib + u < m) psi += (sc[u] < 0.0) ? sc[u] : 0.0;
+        }
         ctl->ss = 0.0;
         ctl->ip = 0;
         if (fabs(psi) <= (double)m * kEps * ctl->c1 * ctl->c2 * 100.0) {
           ctl->phase = PH_DONE;
         } else {
-          for (int i = 0; i < ctl->iq; i++) {
-            uo[i] = uv[i];
-            Ao[i] = Av[i];
-          }
           ctl->phase = PH_SELECT;
         }
       }
       for (int i = ls; i < n; i += S) xo[i] = xv[i];
       grp_sync<S>();
       tph[0] += clk() - t0;
-      continue;
+      if (!QPGPU_WAVE_FALLTHRU) continue;
+      phase = ctl->phase;
     }
     if (phase == PH_SELECT) {
       const uint64_t t0 = clk();
       // ---- l2 (ss deliberately not reset: reference quirk)
+      [[maybe_unused]] double sbest = inf;
+      [[maybe_unused]] int ibest = INT_MAX;
+      if constexpr (kLaneSel) {
+        // each lane scans its constraints in index order, then the subgroup argmin: the same
+        // (smallest s below the carried ss, first index) as the reference's sequential scan
+        const double ss0 = ctl->ss;
+        for (int i = ls; i < m; i += S) {
+          const double v = sv[i];
+          if (v < ss0 && !act[i] && !exc[i] && v < sbest) {
+            sbest = v;
+            ibest = i;
+          }
+        }
+        sg_argmin<S>(sbest, ibest);
+      }
       if (lead) {
         double ss = ctl->ss;
         int ip = ctl->ip;
-        for (int i = 0; i < m; i++)
-          if (sv[i] < ss && !act[i] && !exc[i]) {
-            ss = sv[i];
-            ip = i;
+        if constexpr (kLaneSel) {
+          if (ibest != INT_MAX) {
+            ss = sbest;
+            ip = ibest;
           }
+        } else {
+          for (int i = 0; i < m; i++)
+            if (sv[i] < ss && !act[i] && !exc[i]) {
+              ss = sv[i];
+              ip = i;
+            }
+        }
         ctl->ss = ss;
         ctl->ip = ip;
         if (ss >= 0.0) {
@@ -961,8 +1132,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
         grp_sync<S>();
       }
       tph[1] += clk() - t0;
-      continue;
+      if (!QPGPU_WAVE_FALLTHRU) continue;
+      phase = ctl->phase;
     }
+    if (phase != PH_STEP) continue;
     // ---- l2a (phase == PH_STEP)
     if (lead) {
       if (max_steps > 0 && ++ctl->steps > max_steps) {
@@ -978,15 +1151,37 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
     tph[2] += t1c - t0;
     int kind = 0;  // 1 infeasible, 2 dual step, 3 full step, 4 partial step
     update_r(ctl->iq);
+    // t1 = min over active inequalities with r > 0 of u/r (first index on ties), l its constraint
+    [[maybe_unused]] double t1best = inf;
+    [[maybe_unused]] int kbest = INT_MAX;
+    if constexpr (kLaneSel) {
+      const int iq = ctl->iq;
+      for (int k = p + ls; k < iq; k += S)
+        if (rv[k] > 0.0) {
+          const double q = uv[k] / rv[k];
+          if (q < t1best) {
+            t1best = q;
+            kbest = k;
+          }
+        }
+      sg_argmin<S>(t1best, kbest);
+    }
     if (lead) {
       const int iq = ctl->iq;
       int l = 0;
       double t1 = inf;
-      for (int k = p; k < iq; k++)
-        if (rv[k] > 0.0 && uv[k] / rv[k] < t1) {
-          t1 = uv[k] / rv[k];
-          l = Av[k];
+      if constexpr (kLaneSel) {
+        if (kbest != INT_MAX) {
+          t1 = t1best;
+          l = Av[kbest];
         }
+      } else {
+        for (int k = p; k < iq; k++)
+          if (rv[k] > 0.0 && uv[k] / rv[k] < t1) {
+            t1 = uv[k] / rv[k];
+            l = Av[k];
+          }
+      }
       double t2, zz, znp;
       dot2_lead(zz, znp);
       if (fabs(zz) > kEps) {
@@ -1006,13 +1201,11 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
         ctl->phase = PH_DONE;
         kind = 1;
       } else if (t2 >= inf) {
-        for (int k = 0; k < iq; k++) uv[k] -= t * rv[k];
-        uv[iq] += t;
+        uv[iq] += t;  // u[:iq] -= t r[:iq] by the lanes below
         act[l] = 0;
         kind = 2;
       } else {
         ctl->f += t * znp * (0.5 * t + uv[iq]);
-        for (int k = 0; k < iq; k++) uv[k] -= t * rv[k];
         uv[iq] += t;
         kind = (fabs(t - t2) < kEps) ? 3 : 4;
       }
@@ -1020,6 +1213,11 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
     }
     grp_sync<S>();
     kind = ctl->qq;
+    if (kind >= 2) {
+      const double t = ctl->t;
+      for (int k = ls; k < ctl->iq; k += S) uv[k] -= t * rv[k];
+      grp_sync<S>();
+    }
     t0 = clk();
     tph[3] += t0 - t1c;
     if (kind == 1) continue;
@@ -1044,15 +1242,15 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
         if (lead) exc[ip] = 1;
         grp_sync<S>();
         delete_constraint(ip);
-        if (lead) {
-          for (int i = 0; i < m; i++) act[i] = 0;
-          for (int i = p; i < ctl->iq; i++) {
-            Av[i] = Ao[i];
-            uv[i] = uo[i];
-            act[Av[i]] = 1;
-          }
-          ctl->phase = PH_SELECT;
+        for (int i = ls; i < m; i += S) act[i] = 0;
+        grp_sync<S>();
+        for (int i = p + ls; i < ctl->iq; i += S) {
+          const int ai = Ao[i];
+          Av[i] = ai;
+          uv[i] = uo[i];
+          act[ai] = 1;
         }
+        if (lead) ctl->phase = PH_SELECT;
         for (int i = ls; i < n; i += S) xv[i] = xo[i];
       } else {
         if (lead) {
@@ -1072,8 +1270,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
       tph[5] += clk() - td;
     }
     if (lead) {
-      const double s = seq_fma_up<kUL>(0.0, 0, n, [&](int k) { return npv[k]; },
-                                  [&](int k) { return xv[k]; });
+      const double s = seq_fma_up<8>(0.0, 0, n, [&](int k) { return npv[k]; },
+                                [&](int k) { return xv[k]; });
       sv[ctl->ip] = s + ctl->ci0ip;
       ctl->phase = PH_STEP;
     }

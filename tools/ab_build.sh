@@ -1,7 +1,8 @@
 #!/bin/bash
-# Build an A/B variant of libqpgpu.so with extra -D flags for qp_lane.hip (the other objects are
-# the in-tree build's) into _ab/<name>/libqpgpu.so; register / scratch figures of the lane
-# kernels go to _ab/<name>/regs.txt.   usage: tools/ab_build.sh NAME -DFLAG=V ...
+# Build an A/B variant of libqpgpu.so with extra -D flags for one kernel source (SRC, default
+# qp_lane; the other objects are the in-tree build's) into _ab/<name>/libqpgpu.so; register /
+# scratch figures of that source's kernels go to _ab/<name>/regs.txt.
+#   usage: [SRC=qp_wave] tools/ab_build.sh NAME -DFLAG=V ...
 set -e
 NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -9,10 +10,12 @@ PKG=$ROOT/motion-generation-using-quadratic-programs_amd
 OUT=$ROOT/_ab/$NAME
 rm -rf "$OUT"; mkdir -p "$OUT/tmp"
 make -s -C "$PKG" lib/libqpgpu.so
-for f in qp_layout qp_small qp_wave qp_panel qpgpu_api; do cp "$PKG/lib/$f.o" "$OUT/"; done
+SRC=${SRC:-qp_lane}
+for f in qp_layout qp_lane qp_small qp_wave qp_panel qpgpu_api; do [ "$f" = "$SRC" ] || cp "$PKG/lib/$f.o" "$OUT/"; done
 (cd "$OUT/tmp" && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-fast-math -fPIC \
-   -std=c++17 -I"$ROOT/include" "$@" -c "$PKG/csrc/qp_lane.hip" -o "$OUT/qp_lane.o" -save-temps 2>&1 | grep -v warning | grep -v "warnings\? generated" || true)
+   -std=c++17 -I"$ROOT/include" "$@" -c "$PKG/csrc/$SRC.hip" -o "$OUT/$SRC.o" -save-temps 2>&1 | grep -v warning | grep -v "warnings\? generated" || true)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libqpgpu.so" "$OUT"/*.o
-python3 "$ROOT/tools/kernel_regs.py" "$OUT"/tmp/qp_lane-hip-amdgcn-amd-amdhsa-gfx950.s qp_lane_kernelILi7ELi14ELi1ELb1ELi64 > "$OUT/regs.txt"
+if [ "$SRC" = qp_lane ]; then PAT=qp_lane_kernelILi7ELi14ELi1ELb1ELi64; else PAT=${SRC}_kernel; fi
+python3 "$ROOT/tools/kernel_regs.py" "$OUT/tmp/$SRC-hip-amdgcn-amd-amdhsa-gfx950.s" "$PAT" > "$OUT/regs.txt"
 rm -rf "$OUT/tmp"
 cat "$OUT/regs.txt"

@@ -63,9 +63,9 @@ for s in $STEPS; do
     ab)
       # A/B of the in-tree build against _ab/<variant>/libqpgpu.so (tools/ab_build.sh), per config
       for c in ${CONFIGS:-C1 C2}; do
-        run bench_${c}_base 600 python bench.py --config $c --no-cpu --steps 30
+        run bench_${c}_base 600 python bench.py --config $c --no-cpu --steps ${ABSTEPS:-30}
         for v in ${VARIANTS}; do
-          QPGPU_LIB_PATH=_ab/$v/libqpgpu.so run bench_${c}_$v 600 python bench.py --config $c --no-cpu --steps 30
+          QPGPU_LIB_PATH=_ab/$v/libqpgpu.so run bench_${c}_$v 600 python bench.py --config $c --no-cpu --steps ${ABSTEPS:-30}
         done
       done ;;
     abpar)
@@ -83,6 +83,9 @@ for s in $STEPS; do
       run bench_C3 600 python bench.py --config C3 --no-cpu --steps 10 --warmup 3
       run bench_mgqp 600 python bench.py --config mgqp --no-cpu --steps 20
       run stamps_C3 300 python tools/stamps_wave.py 30 6 60 65536 ;;
+    abwstamps)
+      run wstamps_base 300 python tools/stamps_wave.py ${WSHAPE:-30 6 60 65536}
+      for v in ${VARIANTS}; do QPGPU_LIB_PATH=_ab/$v/libqpgpu.so run wstamps_$v 300 python tools/stamps_wave.py ${WSHAPE:-30 6 60 65536}; done ;;
     listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;
     sq)
       for f in ${FAMILIES:-lane subgroup}; do
