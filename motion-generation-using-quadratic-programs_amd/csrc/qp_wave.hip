@@ -137,7 +137,7 @@ __device__ __forceinline__ double seq_fms_down(double s, int k0, int k1, FA A, F
   return s;
 }
 
-// Value of v held by lane i of this thread's subgroup (S = 32: lanes i and 32 + i of the wave
+// Value of v held by lane i of this thread's subgroup (S = 16 / 32: lane i of each 16- / 32-lane group of the wave
 // serve the two QPs; S = 64: lane i).  i must be wave-uniform (a compile-time step index): two
 // or four v_readlane per double, no LDS round trip.
 template <int S>
@@ -147,8 +147,16 @@ __device__ __forceinline__ double sg_bcast(double v, int i) {
   const uint32_t l0 = __builtin_amdgcn_readlane(lo, i), h0 = __builtin_amdgcn_readlane(hi, i);
   if constexpr (S == 64) {
     return __builtin_bit_cast(double, ((uint64_t)h0 << 32) | l0);
+  } else if constexpr (S == 16) {
+    const uint32_t l1 = __builtin_amdgcn_readlane(lo, 16 + i), h1 = __builtin_amdgcn_readlane(hi, 16 + i);
+    const uint32_t l2 = __builtin_amdgcn_readlane(lo, 32 + i), h2 = __builtin_amdgcn_readlane(hi, 32 + i);
+    const uint32_t l3 = __builtin_amdgcn_readlane(lo, 48 + i), h3 = __builtin_amdgcn_readlane(hi, 48 + i);
+    const int q = threadIdx.x >> 4;
+    const uint32_t l = q == 0 ? l0 : q == 1 ? l1 : q == 2 ? l2 : l3;
+    const uint32_t h = q == 0 ? h0 : q == 1 ? h1 : q == 2 ? h2 : h3;
+    return __builtin_bit_cast(double, ((uint64_t)h << 32) | l);
   } else {
-    static_assert(S == 32, "sg_bcast: one or two QPs per wave");
+    static_assert(S == 32, "sg_bcast: one, two or four QPs per wave");
     const uint32_t l1 = __builtin_amdgcn_readlane(lo, 32 + i), h1 = __builtin_amdgcn_readlane(hi, 32 + i);
     const bool up = threadIdx.x >= 32;
     return __builtin_bit_cast(double, ((uint64_t)(up ? h1 : h0) << 32) | (up ? l1 : l0));
@@ -182,6 +190,10 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
 // once (kScanWide)
 // l1 scan with all of a lane's CI loads issued at once (buffer loads): measured slower (C3
 // 16.0 vs 15.3 ms, scan 196k vs 144k cycles per block, profiles/r02_s10): off
+// four QPs per wave (S = 16) for n <= 16, m <= 32 (the mgqp hierarchy levels)
+#ifndef QPGPU_WAVE_S16
+#define QPGPU_WAVE_S16 1
+#endif
 #ifndef QPGPU_WAVE_FALLTHRU
 #define QPGPU_WAVE_FALLTHRU 1
 #endif
@@ -243,7 +255,8 @@ template <int S, int NMAX, int MMAX, bool GJR, int OCC = 1>
 __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
     qp_wave_kernel(const QpArgs a, double* __restrict__ ws) {
   using C = WaveCfg<S, NMAX, MMAX, GJR>;
-  constexpr bool kRegSetup = QPGPU_WAVE_REGSETUP && !GJR && S == 32 && NMAX <= 32 && OCC == 1;
+  constexpr bool kRegSetup = QPGPU_WAVE_REGSETUP && !GJR && NMAX <= S &&
+                             ((S == 32 && OCC == 1) || (S == 16 && OCC <= 2));
   // lane-parallel selections (argmin of s for l2, of u/r for t1) for one-wave subgroups
   constexpr bool kLaneSel = S <= 64;
   // the one-wave-per-SIMD variant keeps each lane's CI columns (and ci0) in registers from the
@@ -1316,6 +1329,12 @@ static hipError_t launch_wave(const QpArgs& a, hipStream_t stream, double* ws) {
                          lds_bytes, stream, a, ws);
       return hipGetLastError();
     }
+    // four-QP waves (S = 16): up to 40 KiB per block still leaves room for two waves per SIMD
+    if (S == 16 && lds_bytes <= 40960) {
+      hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR, 2>), dim3((unsigned)blocks), dim3(C::BS),
+                         lds_bytes, stream, a, ws);
+      return hipGetLastError();
+    }
   }
   static size_t granted = 0;  // dynamic LDS beyond 64 KiB must be granted per kernel
   if (lds_bytes > 65536 && lds_bytes > granted) {
@@ -1338,6 +1357,9 @@ struct WaveVariant {
 };
 
 static const WaveVariant kWaveVariants[] = {
+#if QPGPU_WAVE_S16
+    {16, 32, 0, "qp_wave<S=16,N=16,M=32>", launch_wave<16, 16, 32, false>},
+#endif
     {32, 64, 0, "qp_wave<S=32,N=32,M=64>", launch_wave<32, 32, 64, false>},
     {32, 128, 0, "qp_wave<S=32,N=32,M=128>", launch_wave<32, 32, 128, false>},
     {64, 128, 0, "qp_wave<S=64,N=64,M=128>", launch_wave<64, 64, 128, false>},
