@@ -37,6 +37,10 @@ __device__ __forceinline__ void grp_sync() {
 #ifndef QPGPU_WAVE_KUL
 #define QPGPU_WAVE_KUL 4
 #endif
+// J columns of a Givens sweep loaded per chunk (LDS-resident J)
+#ifndef QPGPU_WAVE_KUJ
+#define QPGPU_WAVE_KUJ 4
+#endif
 constexpr int kUG = 8, kUL = QPGPU_WAVE_KUL;
 
 // s + sum_{j=j0}^{j1-1} A(j) * B(j), j ascending (s += a*b per element).  Full chunks of kU
@@ -591,6 +595,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
   qp_stamp(a, 2);
   // ------------------------------------------------------------------ shared kernels
   // d = J^T np (lane = column, j ascending); z = J[:, iq:] d[iq:] (lane = row)
+  // diagnostic clocks (stamps only): loop phases (scan, select, d/z, lead step, add, delete) and
+  // equality-phase parts (d/z, update_r, lead t2 + x/u, add_constraint, the lead's |h| chains)
+  uint64_t tph[6] = {0, 0, 0, 0, 0, 0}, teq[5] = {0, 0, 0, 0, 0};
+  auto clk = [&]() -> uint64_t { return a.stamps ? __builtin_amdgcn_s_memtime() : 0; };
   auto compute_d_z = [&](int iq) {
     for (int c = ls; c < n; c += S)
       dv[c] = seq_fma_up<GJR ? KG : kUL>(0.0, 0, n, [&](int j) { return J_(j, c); }, [&](int j) { return npv[j]; });
@@ -690,6 +698,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
   //     R[:iq, iq-1] = d and the degeneracy test.  Returns through ctl->fin (1 = added).
   static_assert(S >= NMAX, "one lane per rotation");
   auto add_constraint = [&]() {
+    const uint64_t h0 = clk();
     if (lead) {
       const int iq = ctl->iq;
       int ng = 0;
@@ -716,6 +725,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
       ctl->ngiv = ng;
     }
     grp_sync<S>();
+    teq[4] += clk() - h0;
     {
       const int ng = ctl->ngiv, g = ls;
       const bool mine = g < ng;
@@ -756,27 +766,34 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
       // Row k's sweep over columns n-1 .. iq: rotation g maps (J[k][j-1], J[k][j]), j = n-1-g,
       // to (n1, xny (t1 + n1) - t2) and n1 is the next rotation's t2, so it is carried in a
       // register and the t1 loads (independent of the chain) are issued kU at a time.
-      constexpr int kU = GJR ? KG : 2;
+      constexpr int kU = GJR ? KG : QPGPU_WAVE_KUJ;
       const int ng = ctl->ngiv;
       for (int k = ls; k < n; k += S) {
         double carry = J_(k, n - 1);
         for (int gb = 0; gb < ng; gb += kU) {
-          double t1v[kU];
+          // the chunk's J entries and rotation coefficients are loaded before its first store
+          // (LDS stores would otherwise fence every later load)
+          double t1v[kU], cv[kU], sw[kU], xw[kU];
+          bool fw[kU];
 #pragma unroll
-          for (int u = 0; u < kU; u++) t1v[u] = (gb + u < ng) ? J_(k, n - 2 - gb - u) : 0.0;
+          for (int u = 0; u < kU; u++) {
+            const int g = gb + u;
+            const bool ok = g < ng;
+            t1v[u] = ok ? J_(k, n - 2 - g) : 0.0;
+            cv[u] = ok ? gc[g] : 0.0;
+            sw[u] = ok ? gs[g] : 0.0;
+            xw[u] = ok ? gx[g] : 0.0;
+            fw[u] = ok && gf[g] != 0.0;
+          }
 #pragma unroll
           for (int u = 0; u < kU; u++) {
             const int g = gb + u;
             if (g < ng) {
               const double t1 = t1v[u], t2 = carry;
-              if (gf[g] != 0.0) {
-                const double n1 = t1 * gc[g] + t2 * gs[g];
-                J_(k, n - 1 - g) = gx[g] * (t1 + n1) - t2;
-                carry = n1;
-              } else {  // skipped step: both columns unchanged
-                J_(k, n - 1 - g) = t2;
-                carry = t1;
-              }
+              const double n1 = t1 * cv[u] + t2 * sw[u];
+              // skipped step (gf = 0): both columns unchanged
+              J_(k, n - 1 - g) = fw[u] ? xw[u] * (t1 + n1) - t2 : t2;
+              carry = fw[u] ? n1 : t1;
             }
           }
         }
@@ -876,27 +893,31 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
     {
       // row k's sweep over columns qq .. qq+ng: rotation g maps (J[k][j], J[k][j+1]), j = qq+g,
       // to (n1, xny (n1 + t1) - t2); the second is the next rotation's t1 (carried)
-      constexpr int kU = GJR ? KG : 2;
+      constexpr int kU = GJR ? KG : QPGPU_WAVE_KUJ;
       const int ng = ctl->ngiv, qq = ctl->qq;
       for (int k = ls; k < n; k += S) {
         double carry = J_(k, qq);
         for (int gb = 0; gb < ng; gb += kU) {
-          double t2v[kU];
+          double t2v[kU], cv[kU], sw[kU], xw[kU];
+          bool fw[kU];
 #pragma unroll
-          for (int u = 0; u < kU; u++) t2v[u] = (gb + u < ng) ? J_(k, qq + gb + u + 1) : 0.0;
+          for (int u = 0; u < kU; u++) {
+            const int g = gb + u;
+            const bool ok = g < ng;
+            t2v[u] = ok ? J_(k, qq + g + 1) : 0.0;
+            cv[u] = ok ? gc[g] : 0.0;
+            sw[u] = ok ? gs[g] : 0.0;
+            xw[u] = ok ? gx[g] : 0.0;
+            fw[u] = ok && gf[g] != 0.0;
+          }
 #pragma unroll
           for (int u = 0; u < kU; u++) {
             const int g = gb + u;
             if (g < ng) {
               const double t1 = carry, t2 = t2v[u];
-              if (gf[g] != 0.0) {
-                const double n1 = t1 * gc[g] + t2 * gs[g];
-                J_(k, qq + g) = n1;
-                carry = gx[g] * (n1 + t1) - t2;
-              } else {
-                J_(k, qq + g) = t1;
-                carry = t2;
-              }
+              const double n1 = t1 * cv[u] + t2 * sw[u];
+              J_(k, qq + g) = fw[u] ? n1 : t1;
+              carry = fw[u] ? xw[u] * (n1 + t1) - t2 : t2;
             }
           }
         }
@@ -908,16 +929,30 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
 
   // ------------------------------------------------------------------ equality phase
   if (chol_ok) {
+    // step i+1's column of CE (lane j: CE[j][i+1]) and ce0[i+1] are loaded during step i, so no
+    // step waits on global memory (S >= NMAX: at most one row per lane)
+    double np_next = (ls < n && p > 0) ? EL(CEb, ls * p) : 0.0;
+    double c0_next = (p > 0) ? EL(ce0b, 0) : 0.0;
     for (int i = 0; i < p; i++) {
-      for (int j = ls; j < n; j += S) npv[j] = EL(CEb, j * p + i);
+      if (ls < n) npv[ls] = np_next;
+      const double c0 = c0_next;
+      if (i + 1 < p) {
+        np_next = ls < n ? EL(CEb, ls * p + i + 1) : 0.0;
+        c0_next = EL(ce0b, i + 1);
+      }
       grp_sync<S>();
+      const uint64_t e0 = clk();
       compute_d_z(ctl->iq);
+      const uint64_t e1 = clk();
       update_r(ctl->iq);
+      const uint64_t e2 = clk();
+      teq[0] += e1 - e0;
+      teq[1] += e2 - e1;
       if (lead) {
         const int iq = ctl->iq;
         double t2 = 0.0, zz, znp;
         dot2_lead(zz, znp);
-        if (fabs(zz) > kEps) t2 = (-dot_lead(npv, xv) - EL(ce0b, i)) / znp;
+        if (fabs(zz) > kEps) t2 = (-dot_lead(npv, xv) - c0) / znp;
         ctl->t2 = t2;
         uv[iq] = t2;
         ctl->f += 0.5 * (t2 * t2) * znp;
@@ -929,7 +964,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
         for (int k = ls; k < n; k += S) xv[k] += t2 * zv[k];
         for (int k = ls; k < ctl->iq; k += S) uv[k] -= t2 * rv[k];
       }
+      const uint64_t e3 = clk();
+      teq[2] += e3 - e2;
       add_constraint();
+      teq[3] += clk() - e3;
       if (!ctl->fin) {
         if (lead) {
           ctl->status = QPGPU_QP_DEPENDENT;
@@ -959,11 +997,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
   // ------------------------------------------------------------------ active-set loop
   // Per-subgroup state machine; a wave loops until all of its QPs are done.
   const int max_steps = a.max_steps;
-  // diagnostic phase clocks (stamps only): scan, select, d/z, lead step, add, delete
-  uint64_t tph[6] = {0, 0, 0, 0, 0, 0};
   [[maybe_unused]] double cir[kCU][kCiReg ? NMAX : 1], c0r[kCU];
   [[maybe_unused]] bool ci_in_regs = false;
-  auto clk = [&]() -> uint64_t { return a.stamps ? __builtin_amdgcn_s_memtime() : 0; };
   // A QP falls through scan -> select -> step within one pass of the loop (QPGPU_WAVE_FALLTHRU),
   // so two QPs of a wave at different phases share the later blocks instead of running them in
   // separate passes.
@@ -1296,6 +1331,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
   qp_stamp(a, 4);
   if (a.stamps && threadIdx.x == 0)
     for (int k = 0; k < 6; k++) a.stamps[(uint64_t)blockIdx.x * kStampSlots + 8 + k] = tph[k];
+  if (a.stamps && threadIdx.x == 0) {
+    for (int k = 0; k < 3; k++) a.stamps[(uint64_t)blockIdx.x * kStampSlots + 5 + k] = teq[k];
+    for (int k = 3; k < 5; k++) a.stamps[(uint64_t)blockIdx.x * kStampSlots + 11 + k] = teq[k];
+  }
   // ------------------------------------------------------------------ outputs
   if (live) {
     const int st = ctl->status;
