@@ -86,6 +86,13 @@ for s in $STEPS; do
     abwstamps)
       run wstamps_base 300 python tools/stamps_wave.py ${WSHAPE:-30 6 60 65536}
       for v in ${VARIANTS}; do QPGPU_LIB_PATH=_ab/$v/libqpgpu.so run wstamps_$v 300 python tools/stamps_wave.py ${WSHAPE:-30 6 60 65536}; done ;;
+    sqcfg)
+      # SQ counters of one config's kernel (CFG, default C3): instruction mix and issue share
+      c=${CFG:-C3}
+      run sqA_$c 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d "$OUT/sqA_$c" -o c1 -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu --streams 1 --kernel-reps 1
+      run sqB_$c 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d "$OUT/sqB_$c" -o c1 -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu --streams 1 --kernel-reps 1
+      run sqC_$c 600 rocprofv3 --pmc SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH --output-format csv -d "$OUT/sqC_$c" -o c1 -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu --streams 1 --kernel-reps 1
+      python3 tools/sqsum.py "$OUT" > "$OUT/sqsum_$c.log" 2>&1; cat "$OUT/sqsum_$c.log" ;;
     listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;
     sq)
       for f in ${FAMILIES:-lane subgroup}; do
