@@ -15,6 +15,7 @@
 // with GJR, J and R live in a global workspace instead (n = 256: 2 x 514 KiB per QP).  The
 // lead lane exchanges scalars with its subgroup through an LDS control block.
 #include <climits>
+#include <cstdlib>
 
 #include "qp_common.h"
 
@@ -207,6 +208,13 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
 #ifndef QPGPU_WAVE_CIREG
 #define QPGPU_WAVE_CIREG 0
 #endif
+// J in registers (one row per lane) with packed R and compute_d through an LDS transpose, for
+// two waves per SIMD: correct (parity green) but measured slower (profiles/r02_s19: C3 18.7 vs
+// 14.5 ms — the S = 32 kernel spills at 256 VGPRs — and mgqp 1.96 vs 1.76 ms — the transposed
+// compute_d doubles d/z), so off
+#ifndef QPGPU_WAVE_REGJ
+#define QPGPU_WAVE_REGJ 0
+#endif
 #ifndef QPGPU_WAVE_REGSETUP
 #define QPGPU_WAVE_REGSETUP 1
 #endif
@@ -238,19 +246,62 @@ struct WaveCfg {
 // (lane = row) are LDS-bank-conflict free; with GJR they live in the workspace instead.
 // Vectors: x z d np r x_old gc gs gx gf (n each), u u_old (n+1 each), s (m), then int A A_old
 // (n+1 each), uint8 act exc (m each) and the control block.
+//
+// REGJ layout (J in registers, one row per lane; see kRegJ): R packed (upper triangle row by row,
+// then the first subdiagonal, then one write-only slot for the entries below it, which the
+// algorithm only ever shifts as zeros), the compute_d transpose scratch [n][kCHS], the loop's
+// vectors, and x z d last — during the setup the factor L ([n][js], rows stride js) overlays
+// everything before x, which is dead until the loop.
+constexpr int kCH = 8, kCHS = kCH + 1;  // compute_d columns per transpose chunk, scratch row stride
 struct WaveLay {
-  int js, off_r, off_x, off_a, off_fl, off_ctl, stride;
+  int js, nr, off_r, off_sc, off_x, off_z, off_d, off_np, off_rv, off_xo, off_gc, off_u, off_uo, off_s,
+      off_a, off_fl, off_ctl, stride;
 };
-__host__ __device__ inline WaveLay wave_lay(int n, int m, bool gjr) {
+__host__ __device__ inline WaveLay wave_lay(int n, int m, bool gjr, bool regj = false) {
   WaveLay L;
   L.js = (n + 1) | 1;
-  L.off_r = gjr ? 0 : n * L.js;
-  L.off_x = gjr ? 0 : 2 * n * L.js;
-  L.off_a = L.off_x + 10 * n + 2 * (n + 1) + m;
-  L.off_fl = L.off_a + (2 * (n + 1) + 1) / 2;
-  L.off_ctl = L.off_fl + (2 * m + 7) / 8;
+  L.nr = n * (n + 1) / 2 + (n > 0 ? n - 1 : 0) + 1;
+  if (!regj) {
+    L.off_r = gjr ? 0 : n * L.js;
+    L.off_sc = L.off_r;
+    L.off_x = gjr ? 0 : 2 * n * L.js;
+    L.off_z = L.off_x + n;
+    L.off_d = L.off_z + n;
+    L.off_np = L.off_d + n;
+    L.off_rv = L.off_np + n;
+    L.off_xo = L.off_rv + n;
+    L.off_gc = L.off_xo + n;
+    L.off_u = L.off_gc + 4 * n;
+    L.off_uo = L.off_u + n + 1;
+    L.off_s = L.off_uo + n + 1;
+    L.off_a = L.off_s + m;
+    L.off_fl = L.off_a + (2 * (n + 1) + 1) / 2;
+    L.off_ctl = L.off_fl + (2 * m + 7) / 8;
+  } else {
+    L.off_r = 0;
+    L.off_sc = L.nr;
+    L.off_np = L.off_sc + n * kCHS;
+    L.off_rv = L.off_np + n;
+    L.off_xo = L.off_rv + n;
+    L.off_gc = L.off_xo + n;
+    L.off_u = L.off_gc + 4 * n;
+    L.off_uo = L.off_u + n + 1;
+    L.off_s = L.off_uo + n + 1;
+    L.off_a = L.off_s + m;
+    L.off_fl = L.off_a + (2 * (n + 1) + 1) / 2;
+    const int end = L.off_fl + (2 * m + 7) / 8;
+    L.off_x = end > n * L.js ? end : n * L.js;
+    L.off_z = L.off_x + n;
+    L.off_d = L.off_z + n;
+    L.off_ctl = L.off_d + n;
+  }
   L.stride = (L.off_ctl + (int)((sizeof(Ctl) + 7) / 8)) | 1;
   return L;
+}
+// packed-R index (REGJ): R[i][j] for j >= i, the subdiagonal R[j+1][j], else the write-only slot
+__device__ __forceinline__ int rpk(int i, int j, int n) {
+  const int nup = n * (n + 1) / 2;
+  return j >= i ? i * n - (i * (i - 1)) / 2 + (j - i) : (i == j + 1 ? nup + j : nup + n - 1);
 }
 
 // OCC = minimum waves per SIMD the register allocation must allow (launch-bounds hint): 1, or
@@ -259,8 +310,11 @@ template <int S, int NMAX, int MMAX, bool GJR, int OCC = 1>
 __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
     qp_wave_kernel(const QpArgs a, double* __restrict__ ws) {
   using C = WaveCfg<S, NMAX, MMAX, GJR>;
+  // J in registers (lane r holds row r) and R packed, so a two-QP block of C3 fits 20 KiB of LDS
+  // and two waves run on every SIMD (launched at OCC = 2)
+  constexpr bool kRegJ = QPGPU_WAVE_REGJ && !GJR && S <= 32 && NMAX <= S && OCC == 2;
   constexpr bool kRegSetup = QPGPU_WAVE_REGSETUP && !GJR && NMAX <= S &&
-                             ((S == 32 && OCC == 1) || (S == 16 && OCC <= 2));
+                             ((S == 32 && OCC == 1) || (S == 16 && OCC <= 2) || kRegJ);
   // lane-parallel selections (argmin of s for l2, of u/r for t1) for one-wave subgroups
   constexpr bool kLaneSel = S <= 64;
   // the one-wave-per-SIMD variant keeps each lane's CI columns (and ci0) in registers from the
@@ -274,7 +328,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
   // workspace variant, whose lanes have registers to spare)
   constexpr int KG = GJR ? 16 : kUG;
   extern __shared__ double lds[];
-  const WaveLay Ly = wave_lay(a.n, a.m, GJR);
+  const WaveLay Ly = wave_lay(a.n, a.m, GJR, kRegJ);
   const int JS = GJR ? BigWs<NMAX>::JS : Ly.js;
 
   const int tid = threadIdx.x;
@@ -287,20 +341,22 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
   double* const Q = lds + sg * Ly.stride;
   double* const Jm = GJR ? ws + (b < a.batch ? b : 0) * (int64_t)C::WS_DOUBLES : Q;
   double* const Rm = GJR ? Jm + BigWs<NMAX>::OFF_R : Q + Ly.off_r;
+  double* const Lm = kRegJ ? Q : Rm;  // the factor L during the setup ([n][js])
+  [[maybe_unused]] double* const sc = Q + Ly.off_sc;  // compute_d transpose scratch (REGJ)
   const int nv = a.n;
   double* const xv = Q + Ly.off_x;
-  double* const zv = xv + nv;
-  double* const dv = zv + nv;
-  double* const npv = dv + nv;
-  double* const rv = npv + nv;
-  double* const xo = rv + nv;
-  double* const gc = xo + nv;
+  double* const zv = Q + Ly.off_z;
+  double* const dv = Q + Ly.off_d;
+  double* const npv = Q + Ly.off_np;
+  double* const rv = Q + Ly.off_rv;
+  double* const xo = Q + Ly.off_xo;
+  double* const gc = Q + Ly.off_gc;
   double* const gs = gc + nv;
   double* const gx = gs + nv;
   double* const gf = gx + nv;  // Givens step applied (1.0) / skipped (0.0)
-  double* const uv = gf + nv;
-  double* const uo = uv + nv + 1;
-  double* const sv = uo + nv + 1;
+  double* const uv = Q + Ly.off_u;
+  double* const uo = Q + Ly.off_uo;
+  double* const sv = Q + Ly.off_s;
   int* const Av = reinterpret_cast<int*>(Q + Ly.off_a);
   int* const Ao = Av + nv + 1;
   uint8_t* const act = reinterpret_cast<uint8_t*>(Q + Ly.off_fl);  // iai[i] == -1
@@ -320,7 +376,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
   // J in LDS: row-major.  J in the workspace (GJR): column-major, so that the row-parallel work
   // (Givens sweeps, update_z, building J) reads and writes it coalesced across lanes.
 #define J_(i, j) (GJR ? Jm[(j) * JS + (i)] : Jm[(i) * JS + (j)])
-#define R_(i, j) Rm[(i) * JS + (j)]
+#define R_(i, j) Rm[kRegJ ? rpk((i), (j), n) : (i) * JS + (j)]
+#define L_(i, j) Lm[(i) * JS + (j)]
+  // J in registers (kRegJ): lane r holds row r, indexed with compile-time column indices only
+  [[maybe_unused]] double Jr[kRegJ ? NMAX : 1];
   // setup already in the workspace (qp_panel.hip): start from its header
   const bool pre = GJR && (a.flags & kSetupDone);
 
@@ -348,7 +407,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
   if (live && !pre) {
     for (int e = ls; e < n * n; e += S) {
       const int i = e / n, j = e - (e / n) * n;
-      R_(i, j) = EL(Gb, e);
+      L_(i, j) = EL(Gb, e);
     }
     for (int i = ls; i < n; i += S) zv[i] = EL(g0b, i);
   }
@@ -372,7 +431,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
     if (live) {
       if (lead) {
         double c1 = 0.0;
-        for (int i = 0; i < n; i++) c1 += R_(i, i);
+        for (int i = 0; i < n; i++) c1 += L_(i, i);
         ctl->c1 = c1;
       }
       const int j = ls;
@@ -380,7 +439,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
       const int jc = mine ? j : n - 1;
       double A[NMAX];
 #pragma unroll
-      for (int k = 0; k < NMAX; k++) A[k] = R_(jc, k < n ? k : n - 1);
+      for (int k = 0; k < NMAX; k++) A[k] = L_(jc, k < n ? k : n - 1);
       bool fail = false;
       double bad = 0.0;
 #pragma unroll
@@ -389,8 +448,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
           const double lnew = i > 0 ? sg_bcast<S>(A[i > 0 ? i - 1 : 0], i) : 0.0;  // L[i][i-1]
           double lold[NMAX];
 #pragma unroll
-          for (int k = 0; k + 1 < i; k++) lold[k] = R_(i, k);
-          double sum = (j == i) ? A[i] : R_(i, jc);
+          for (int k = 0; k + 1 < i; k++) lold[k] = L_(i, k);
+          double sum = (j == i) ? A[i] : L_(i, jc);
 #pragma unroll
           for (int k = i - 1; k >= 0; k--) sum -= ((k == i - 1) ? lnew : lold[k]) * A[k];
           const double sd = sg_bcast<S>(sum, i);
@@ -402,8 +461,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
             const double v = (j == i) ? dg : sum / dg;
             if (mine && j >= i) {
               A[i] = v;
-              R_(j, i) = v;
-              if (j > i) R_(i, j) = v;
+              L_(j, i) = v;
+              if (j > i) L_(i, j) = v;
             }
           }
           sg_sync();
@@ -419,14 +478,14 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
     if (live && !pre) {
       if (lead) {
         double c1 = 0.0;
-        for (int i = 0; i < n; i++) c1 += R_(i, i);
+        for (int i = 0; i < n; i++) c1 += L_(i, i);
         ctl->c1 = c1;
       }
       // cholesky_decomposition (@.text+0x2df0): row-wise, descending-k sums, upper mirrored.
       for (int i = 0; i < n; i++) {
         if (lead) {
-          const double sum = seq_fms_down<GJR ? kUG : kUL>(R_(i, i), 0, i, [&](int k) { return R_(i, k); },
-                                          [&](int k) { return R_(i, k); });
+          const double sum = seq_fms_down<GJR ? kUG : kUL>(L_(i, i), 0, i, [&](int k) { return L_(i, k); },
+                                          [&](int k) { return L_(i, k); });
           if (sum <= 0.0) {
             ctl->status = QPGPU_QP_NOT_POSITIVE_DEFINITE;
             ctl->f = sum;
@@ -438,13 +497,13 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
         if (ctl->status != QPGPU_QP_OK) break;
         const double dg = ctl->t;
         for (int j = i + 1 + ls; j < n; j += S) {
-          const double s2 = seq_fms_down<GJR ? kUG : kUL>(R_(i, j), 0, i, [&](int k) { return R_(i, k); },
-                                         [&](int k) { return R_(j, k); });
-          R_(j, i) = s2 / dg;
+          const double s2 = seq_fms_down<GJR ? kUG : kUL>(L_(i, j), 0, i, [&](int k) { return L_(i, k); },
+                                         [&](int k) { return L_(j, k); });
+          L_(j, i) = s2 / dg;
         }
-        if (lead) R_(i, i) = dg;
+        if (lead) L_(i, i) = dg;
         grp_sync<S>();
-        for (int k = i + 1 + ls; k < n; k += S) R_(i, k) = R_(k, i);
+        for (int k = i + 1 + ls; k < n; k += S) L_(i, k) = L_(k, i);
         grp_sync<S>();
       }
     }
@@ -453,7 +512,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
   const bool chol_ok = live && ctl->status == QPGPU_QP_OK;
   if (live && !pre && (a.flags & QPGPU_FLAG_WRITE_FACTOR)) {
     double* Gw = a.G + qbase_rt(bb, n * n, T);
-    for (int e = ls; e < n * n; e += S) EL(Gw, e) = R_(e / n, e - (e / n) * n);
+    for (int e = ls; e < n * n; e += S) EL(Gw, e) = L_(e / n, e - (e / n) * n);
   }
   if constexpr (kRegSetup) {
     if (chol_ok) {
@@ -472,16 +531,39 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
       double w[NMAX];
 #pragma unroll
       for (int k = 0; k < NMAX; k++) w[k] = (k == j) ? 1.0 : 0.0;
-      for (int q = 0; q < n; q++) {
-        const double* Lq = Rm + q * JS + q;  // Lq[k] = L[q+k][q] (k >= 1), Lq[0] = L[q][q]
-        double lc[NMAX];
+      if constexpr (kRegJ) {
+        // J stays in registers: the outputs shift through Jr as well, so after NMAX steps (those
+        // past n only touch entries past n, which end as +0.0) Jr[k] = y_k at compile-time k
+#pragma unroll 1
+        for (int q = 0; q < NMAX; q++) {
+          const int qc = q < n ? q : n - 1;
+          const double* Lq = Lm + qc * JS + qc;
+          const double y = w[0] / Lq[0];
 #pragma unroll
-        for (int k = 0; k < NMAX; k++) lc[k] = Lq[k];
-        const double y = w[0] / lc[0];
-        if (mine) J_(j, q) = y;
+          for (int k = 0; k + 1 < NMAX; k++) Jr[k] = Jr[k + 1];
+          Jr[NMAX - 1] = y;
 #pragma unroll
-        for (int k = 0; k + 1 < NMAX; k++) w[k] = w[k + 1] - lc[k + 1] * y;
-        w[NMAX - 1] = 0.0;
+          for (int k = 0; k + 1 < NMAX; k++) w[k] = w[k + 1] - Lq[k + 1] * y;
+          w[NMAX - 1] = 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < NMAX; k++) Jr[k] = (mine && k < n) ? Jr[k] : 0.0;
+        double dj = 0.0;  // J[j][j], for c2 = trace(J)
+#pragma unroll
+        for (int k = 0; k < NMAX; k++) dj = (k == j) ? Jr[k] : dj;
+        if (mine) dv[j] = dj;
+      } else {
+        for (int q = 0; q < n; q++) {
+          const double* Lq = Lm + q * JS + q;  // Lq[k] = L[q+k][q] (k >= 1), Lq[0] = L[q][q]
+          double lc[NMAX];
+#pragma unroll
+          for (int k = 0; k < NMAX; k++) lc[k] = Lq[k];
+          const double y = w[0] / lc[0];
+          if (mine) J_(j, q) = y;
+#pragma unroll
+          for (int k = 0; k + 1 < NMAX; k++) w[k] = w[k + 1] - lc[k + 1] * y;
+          w[NMAX - 1] = 0.0;
+        }
       }
       // cholesky_solve (@.text+0x31a2) across the lanes: forward y = L^{-1} g0 column-oriented
       // (lane i accumulates its row's subtractions in q order), backward x = L^{-T} y row by row
@@ -489,17 +571,17 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
       // order, the reference's; entries past n stay +0.0 and subtract nothing).  Row j of the
       // factor array holds both L[j][q] (q < j) and U[j][i] (i > j).  Divisors broadcast with
       // v_readlane.
-      const double diag = R_(jc, jc);
+      const double diag = L_(jc, jc);
       double yv = zv[jc];
       for (int q = 0; q < n; q++) {
-        const double lq = R_(jc, q);
+        const double lq = L_(jc, q);
         const double yq = sg_bcast<S>(yv / diag, q);
         const double upd = yv - lq * yq;
         yv = (j == q) ? yq : ((j > q) ? upd : yv);
       }
       double Lr[NMAX];
 #pragma unroll
-      for (int k = 0; k < NMAX; k++) Lr[k] = R_(jc, k);
+      for (int k = 0; k < NMAX; k++) Lr[k] = L_(jc, k);
       double P[NMAX];
 #pragma unroll
       for (int k = 0; k < NMAX; k++) P[k] = 0.0;
@@ -517,7 +599,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
       grp_sync<S>();
       if (lead) {
         double c2 = 0.0;
-        for (int i = 0; i < n; i++) c2 += J_(i, i);
+        for (int i = 0; i < n; i++) c2 += kRegJ ? dv[i] : J_(i, i);
         ctl->c2 = c2;
         double f = 0.0;
         for (int i = 0; i < n; i++) f += zv[i] * xv[i];
@@ -536,7 +618,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
         int fin = 1;
         for (int i = 0; i < n && fin; i++)
           for (int j = 0; j <= i; j++)
-            if (!(fabs(R_(i, j)) < inf)) {
+            if (!(fabs(L_(i, j)) < inf)) {
               fin = 0;
               break;
             }
@@ -548,9 +630,9 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
         const int i0 = skip ? r : 0;
         for (int i = 0; i < i0; i++) J_(r, i) = 0.0;
         for (int i = i0; i < n; i++) {
-          const double v = seq_fms_up<GJR ? kUG : kUL>((i == r) ? 1.0 : 0.0, i0, i, [&](int j) { return R_(i, j); },
+          const double v = seq_fms_up<GJR ? kUG : kUL>((i == r) ? 1.0 : 0.0, i0, i, [&](int j) { return L_(i, j); },
                                       [&](int j) { return J_(r, j); });
-          J_(r, i) = v / R_(i, i);
+          J_(r, i) = v / L_(i, i);
         }
       }
       grp_sync<S>();
@@ -560,14 +642,14 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
         ctl->c2 = c2;
         // cholesky_solve (@.text+0x31a2): y -> d, x = -G^{-1} g0
         for (int i = 0; i < n; i++) {
-          const double v = seq_fms_up<GJR ? kUG : kUL>(zv[i], 0, i, [&](int j) { return R_(i, j); },
+          const double v = seq_fms_up<GJR ? kUG : kUL>(zv[i], 0, i, [&](int j) { return L_(i, j); },
                                       [&](int j) { return dv[j]; });
-          dv[i] = v / R_(i, i);
+          dv[i] = v / L_(i, i);
         }
         for (int i = n - 1; i >= 0; i--) {
-          const double v = seq_fms_up<GJR ? kUG : kUL>(dv[i], i + 1, n, [&](int j) { return R_(i, j); },
+          const double v = seq_fms_up<GJR ? kUG : kUL>(dv[i], i + 1, n, [&](int j) { return L_(i, j); },
                                       [&](int j) { return xv[j]; });
-          xv[i] = v / R_(i, i);
+          xv[i] = v / L_(i, i);
         }
         double f = 0.0;
         for (int i = 0; i < n; i++) {
@@ -583,7 +665,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
   }
   if (chol_ok) {
     // R = 0 (L no longer needed), flags
-    for (int e = ls; e < n * JS; e += S) Rm[e] = 0.0;
+    for (int e = ls; e < (kRegJ ? Ly.nr : n * JS); e += S) Rm[e] = 0.0;
     for (int i = ls; i < m; i += S) act[i] = exc[i] = 0;
     for (int i = ls; i <= n; i += S) {
       uv[i] = 0.0;
@@ -600,12 +682,57 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
   uint64_t tph[6] = {0, 0, 0, 0, 0, 0}, teq[5] = {0, 0, 0, 0, 0};
   auto clk = [&]() -> uint64_t { return a.stamps ? __builtin_amdgcn_s_memtime() : 0; };
   auto compute_d_z = [&](int iq) {
-    for (int c = ls; c < n; c += S)
-      dv[c] = seq_fma_up<GJR ? KG : kUL>(0.0, 0, n, [&](int j) { return J_(j, c); }, [&](int j) { return npv[j]; });
-    grp_sync<S>();
-    for (int r = ls; r < n; r += S)
-      zv[r] = seq_fma_up<GJR ? KG : kUL>(0.0, iq, n, [&](int j) { return J_(r, j); }, [&](int j) { return dv[j]; });
-    grp_sync<S>();
+    if constexpr (kRegJ) {
+      // d[c] = sum_j J[j][c] np[j] (j ascending) with row j in lane j's registers: the products
+      // J[j][c] np[j] (the reference's roundings) go through the scratch kCH columns at a time,
+      // and lane c adds column c's n products in row order
+      const double npr = ls < n ? npv[ls] : 0.0;
+#pragma unroll
+      for (int c0 = 0; c0 < NMAX; c0 += kCH) {
+        if (c0 < n) {
+          if (ls < n)
+#pragma unroll
+            for (int u = 0; u < kCH; u++)
+              if (c0 + u < NMAX) sc[ls * kCHS + u] = Jr[c0 + u < NMAX ? c0 + u : 0] * npr;
+          grp_sync<S>();
+          const int c = ls - c0;
+          if (c >= 0 && c < kCH && ls < n) {
+            double sd = 0.0;
+            constexpr int U = 8;
+            for (int jb = 0; jb < n; jb += U) {
+              double pv[U];
+#pragma unroll
+              for (int u = 0; u < U; u++) pv[u] = jb + u < n ? sc[(jb + u) * kCHS + c] : 0.0;
+#pragma unroll
+              for (int u = 0; u < U; u++)
+                if (jb + u < n) sd += pv[u];
+            }
+            dv[ls] = sd;
+          }
+          grp_sync<S>();
+        }
+      }
+      // z[r] = sum_{j >= iq} J[r][j] d[j] (j ascending) in lane r's registers; entries below iq
+      // or past n add +0.0 to a sum that starts at +0.0 (never -0.0): no-ops
+      if (ls < n) {
+        double z = 0.0;
+#pragma unroll
+        for (int j = 0; j < NMAX; j++) {
+          const double dj = dv[j < n ? j : 0];
+          z += (j >= iq && j < n) ? Jr[j] * dj : 0.0;
+          if (j % 8 == 7) __builtin_amdgcn_sched_barrier(0);  // d loads 8 at a time (registers)
+        }
+        zv[ls] = z;
+      }
+      grp_sync<S>();
+    } else {
+      for (int c = ls; c < n; c += S)
+        dv[c] = seq_fma_up<GJR ? KG : kUL>(0.0, 0, n, [&](int j) { return J_(j, c); }, [&](int j) { return npv[j]; });
+      grp_sync<S>();
+      for (int r = ls; r < n; r += S)
+        zv[r] = seq_fma_up<GJR ? KG : kUL>(0.0, iq, n, [&](int j) { return J_(r, j); }, [&](int j) { return dv[j]; });
+      grp_sync<S>();
+    }
   };
   // update_r (r = R[:iq,:iq]^{-1} d[:iq], rows i descending, each s = sum_{j>i} R[i][j] r[j]
   // with j ascending).  LDS-resident R: the lead alone.  R in the workspace (GJR): wave 0 works
@@ -762,7 +889,25 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
     }
     grp_sync<S>();
     const int iq0 = ctl->iq;
-    if (iq0 < n) {
+    if (kRegJ && iq0 < n) {
+      // the same sweep on lane k's register row: rotation g = n-1-j on columns (j-1, j), j from
+      // n-1 down to iq+1, with the reference's operations; out-of-range steps leave both columns
+      if (ls < n) {
+#pragma unroll
+        for (int j = NMAX - 1; j >= 1; j--) {
+          const int g = n - 1 - j;
+          const bool on = j <= n - 1 && j >= iq0 + 1;
+          const int gi = on ? g : 0;
+          const double c = gc[gi], sn = gs[gi], xn = gx[gi];
+          const bool f = on && gf[gi] != 0.0;
+          const double t1 = Jr[j - 1], t2 = Jr[j];
+          const double n1 = t1 * c + t2 * sn;
+          Jr[j - 1] = f ? n1 : t1;
+          Jr[j] = f ? xn * (t1 + n1) - t2 : t2;
+          if (j % 4 == 0) __builtin_amdgcn_sched_barrier(0);  // coefficients 4 steps at a time
+        }
+      }
+    } else if (iq0 < n) {
       // Row k's sweep over columns n-1 .. iq: rotation g maps (J[k][j-1], J[k][j]), j = n-1-g,
       // to (n1, xny (t1 + n1) - t2) and n1 is the next rotation's t2, so it is carried in a
       // register and the t1 loads (independent of the chain) are issued kU at a time.
@@ -895,7 +1040,25 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
       // to (n1, xny (n1 + t1) - t2); the second is the next rotation's t1 (carried)
       constexpr int kU = GJR ? KG : QPGPU_WAVE_KUJ;
       const int ng = ctl->ngiv, qq = ctl->qq;
-      for (int k = ls; k < n; k += S) {
+      if constexpr (kRegJ) {
+        // lane k's register row: rotation g = j - qq on columns (j, j+1), j ascending
+        if (ls < n) {
+#pragma unroll
+          for (int j = 0; j + 1 < NMAX; j++) {
+            const int g = j - qq;
+            const bool on = g >= 0 && g < ng;
+            const int gi = on ? g : 0;
+            const double c = gc[gi], sn = gs[gi], xn = gx[gi];
+            const bool f = on && gf[gi] != 0.0;
+            const double t1 = Jr[j], t2 = Jr[j + 1];
+            const double n1 = t1 * c + t2 * sn;
+            Jr[j] = f ? n1 : t1;
+            Jr[j + 1] = f ? xn * (n1 + t1) - t2 : t2;
+            if (j % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+      for (int k = kRegJ ? n : ls; k < n; k += S) {
         double carry = J_(k, qq);
         for (int gb = 0; gb < ng; gb += kU) {
           double t2v[kU], cv[kU], sw[kU], xw[kU];
@@ -1356,7 +1519,15 @@ template <int S, int NMAX, int MMAX, bool GJR>
 static hipError_t launch_wave(const QpArgs& a, hipStream_t stream, double* ws) {
   using C = WaveCfg<S, NMAX, MMAX, GJR>;
   const int64_t blocks = (a.batch + C::QPB - 1) / C::QPB;
-  const size_t lds_bytes = (size_t)C::QPB * wave_lay(a.n, a.m, GJR).stride * sizeof(double);
+  // J in registers (kRegJ): the smaller REGJ layout, two waves per SIMD (C3: 19.8 KiB per
+  // two-QP block, 8 blocks per CU)
+  if constexpr (QPGPU_WAVE_REGJ && S <= 32 && !GJR && NMAX <= S) {
+    const size_t lds_j = (size_t)C::QPB * wave_lay(a.n, a.m, GJR, true).stride * sizeof(double);
+    hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR, 2>), dim3((unsigned)blocks), dim3(C::BS), lds_j,
+                       stream, a, ws);
+    return hipGetLastError();
+  }
+  size_t lds_bytes = (size_t)C::QPB * wave_lay(a.n, a.m, GJR).stride * sizeof(double);
   // Two-QP-per-wave variants: when a block's LDS leaves room for >= 2 waves per SIMD (<= 20 KiB,
   // i.e. >= 8 one-wave blocks per CU) register pressure is the occupancy limit, so launch the
   // instantiation compiled for 4 waves per SIMD (a few spilled VGPRs).  Measured: mgqp level 0
@@ -1373,6 +1544,20 @@ static hipError_t launch_wave(const QpArgs& a, hipStream_t stream, double* ws) {
       hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR, 2>), dim3((unsigned)blocks), dim3(C::BS),
                          lds_bytes, stream, a, ws);
       return hipGetLastError();
+    }
+  }
+  // workspace variant (n > 64): QPGPU_WAVE_GJR_BLOCKS_PER_CU = k pads the dynamic LDS so at most
+  // k one-QP workgroups share a CU (diagnostic: fewer resident QPs = a working set that stays in
+  // the Infinity Cache; 0 = no cap)
+  if constexpr (GJR) {
+    static int cap = -1;
+    if (cap < 0) {
+      const char* e = getenv("QPGPU_WAVE_GJR_BLOCKS_PER_CU");
+      cap = e ? atoi(e) : 0;
+    }
+    if (cap > 0) {
+      const size_t want = (size_t)163840 / (size_t)cap - 1024;
+      if (want > lds_bytes) lds_bytes = want;
     }
   }
   static size_t granted = 0;  // dynamic LDS beyond 64 KiB must be granted per kernel

@@ -93,6 +93,9 @@ for s in $STEPS; do
       run sqB_$c 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d "$OUT/sqB_$c" -o c1 -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu --streams 1 --kernel-reps 1
       run sqC_$c 600 rocprofv3 --pmc SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH --output-format csv -d "$OUT/sqC_$c" -o c1 -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu --streams 1 --kernel-reps 1
       python3 tools/sqsum.py "$OUT" > "$OUT/sqsum_$c.log" 2>&1; cat "$OUT/sqsum_$c.log" ;;
+    c5res)
+      # C5 with the number of resident QPs per CU capped (Infinity-Cache residency experiment)
+      for k in ${CAPS:-1 2 4}; do QPGPU_WAVE_GJR_BLOCKS_PER_CU=$k run bench_C5_cap$k 600 python bench.py --config C5 --no-cpu --steps 2 --warmup 1 --kernel-reps 2; done ;;
     listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;
     sq)
       for f in ${FAMILIES:-lane subgroup}; do
