@@ -22,9 +22,11 @@ re-solved) is reported beside it.
 
 Timing: steps are independent batches, pipelined round-robin over --streams HIP streams (default
 3) with private outputs; `value` is that whole-job throughput.  `value_streams1` is the same K
-steps serialized on one stream.  `roofline` uses the kernel's own duration: serialized launches
-on one stream bracketed by HIP events on that stream (cold rotation), which is what
-`rocprofv3 --kernel-trace --stats -- python bench.py --streams 1` reports.
+steps serialized on one stream.  `roofline` uses the kernel's own duration: --kernel-reps
+serialized launches on one stream between one HIP-event pair on that stream (cold rotation;
+the launch-to-launch average, which includes the dependent-launch gap and sits just above what
+`rocprofv3 --kernel-trace --stats -- python bench.py --streams 1` reports per kernel); the
+average of one event pair per launch is reported beside it.
 
 Single-GPU:  python bench.py [--steps K --warmup W] [--config C1|C2|C3|C4|mgqp|C5]
 Multi-GPU:   python bench.py --gpus N ...   (starts torch.distributed.run with N ranks itself)
@@ -314,27 +316,40 @@ def main():
     # that stream around each launch, rotating over the cold sets (and once more warm)
     cs = streams[0]
 
-    def kernel_ms(rotate):
-        st_ = [torch.cuda.Event(enable_timing=True) for _ in range(args.kernel_reps)]
-        en_ = [torch.cuda.Event(enable_timing=True) for _ in range(args.kernel_reps)]
-        for q in range(args.kernel_reps):
-            fn = launcher(q % R if rotate else 0, 0, cs)
-            st_[q].record(cs)
-            fn()
-            en_[q].record(cs)
+    def kernel_ms(rotate, per_launch=False):
+        # one HIP-event pair around kernel_reps back-to-back launches on one stream (average
+        # launch-to-launch duration: kernel + the dependent-launch gap), or a pair per launch
+        K_ = args.kernel_reps
+        fns = [launcher(q % R if rotate else 0, 0, cs) for q in range(K_)]
+        if per_launch:
+            st_ = [torch.cuda.Event(enable_timing=True) for _ in range(K_)]
+            en_ = [torch.cuda.Event(enable_timing=True) for _ in range(K_)]
+            for q in range(K_):
+                st_[q].record(cs)
+                fns[q]()
+                en_[q].record(cs)
+            torch.cuda.synchronize(dev)
+            return float(np.mean([a_.elapsed_time(b_) for a_, b_ in zip(st_, en_)]))
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(cs)
+        for q in range(K_):
+            fns[q]()
+        e1.record(cs)
         torch.cuda.synchronize(dev)
-        return float(np.mean([a_.elapsed_time(b_) for a_, b_ in zip(st_, en_)]))
+        return e0.elapsed_time(e1) / K_
 
     kern_cold = kernel_ms(True)
     kern_warm = kernel_ms(False)
+    kern_cold_pair = kernel_ms(True, per_launch=True)
 
     gather_ms = gat.time_one() if gat else None  # one step's gather alone, same payload
 
     if dist:
-        t = torch.tensor([elapsed, elapsed1, kern_cold, kern_warm, gather_ms or 0.0],
+        t = torch.tensor([elapsed, elapsed1, kern_cold, kern_warm, gather_ms or 0.0, kern_cold_pair],
                          dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, elapsed1, kern_cold, kern_warm = (float(v) for v in t[:4])
+        kern_cold_pair = float(t[5])
         if gather:
             gather_ms = float(t[4])
         ok_t = torch.tensor([1 if consistent else 0], device=dev if backend == "nccl" else "cpu")
@@ -381,8 +396,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms": kern_cold,
-                     "kernel_ms_source": "serialized launches on one stream, HIP events, inputs "
-                                         f"rotating over {R} resident set(s)",
+                     "kernel_ms_source": f"{args.kernel_reps} serialized launches on one stream "
+                                         "between one HIP-event pair (launch-to-launch average), "
+                                         f"inputs rotating over {R} resident set(s)",
+                     "kernel_ms_event_pair_per_launch": kern_cold_pair,
                      "warm": {"kernel_ms": kern_warm, "achieved": achieved_warm,
                               "frac": achieved_warm / HBM_PEAK_GBS},
                      "algorithmic_bytes_per_qp": bpq,

@@ -306,8 +306,11 @@ __device__ __forceinline__ int rpk(int i, int j, int n) {
 
 // OCC = minimum waves per SIMD the register allocation must allow (launch-bounds hint): 1, or
 // 4 for the two-QP-per-wave variants when the launch's LDS leaves room for that many (launch_wave)
+// The workspace variant (GJR, 256-thread one-QP workgroups) is held to 128 VGPRs (four waves
+// per SIMD = four resident QPs per CU): its loop is bound by HBM traffic, which it overlaps only
+// across resident QPs (measured: two per CU 399 ms, four 323 ms for C5, profiles/r02_f).
 template <int S, int NMAX, int MMAX, bool GJR, int OCC = 1>
-__global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
+__global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
     qp_wave_kernel(const QpArgs a, double* __restrict__ ws) {
   using C = WaveCfg<S, NMAX, MMAX, GJR>;
   // J in registers (lane r holds row r) and R packed, so a two-QP block of C3 fits 20 KiB of LDS
@@ -916,29 +919,40 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
       for (int k = ls; k < n; k += S) {
         double carry = J_(k, n - 1);
         for (int gb = 0; gb < ng; gb += kU) {
-          // the chunk's J entries and rotation coefficients are loaded before its first store
-          // (LDS stores would otherwise fence every later load)
-          double t1v[kU], cv[kU], sw[kU], xw[kU];
-          bool fw[kU];
+          // the chunk's J entries (and, with J in LDS, its rotation coefficients) are loaded
+          // before its first store (LDS stores would otherwise fence every later load); the
+          // workspace variant reads the coefficients per rotation (registers: its occupancy)
+          constexpr int kUC = GJR ? 1 : kU;
+          double t1v[kU], cv[kUC], sw[kUC], xw[kUC];
+          bool fw[kUC];
 #pragma unroll
           for (int u = 0; u < kU; u++) {
             const int g = gb + u;
             const bool ok = g < ng;
             t1v[u] = ok ? J_(k, n - 2 - g) : 0.0;
-            cv[u] = ok ? gc[g] : 0.0;
-            sw[u] = ok ? gs[g] : 0.0;
-            xw[u] = ok ? gx[g] : 0.0;
-            fw[u] = ok && gf[g] != 0.0;
+            if constexpr (!GJR) {
+              cv[u] = ok ? gc[g] : 0.0;
+              sw[u] = ok ? gs[g] : 0.0;
+              xw[u] = ok ? gx[g] : 0.0;
+              fw[u] = ok && gf[g] != 0.0;
+            }
           }
 #pragma unroll
           for (int u = 0; u < kU; u++) {
             const int g = gb + u;
             if (g < ng) {
+              const int uc = GJR ? 0 : u;
+              if constexpr (GJR) {
+                cv[0] = gc[g];
+                sw[0] = gs[g];
+                xw[0] = gx[g];
+                fw[0] = gf[g] != 0.0;
+              }
               const double t1 = t1v[u], t2 = carry;
-              const double n1 = t1 * cv[u] + t2 * sw[u];
+              const double n1 = t1 * cv[uc] + t2 * sw[uc];
               // skipped step (gf = 0): both columns unchanged
-              J_(k, n - 1 - g) = fw[u] ? xw[u] * (t1 + n1) - t2 : t2;
-              carry = fw[u] ? n1 : t1;
+              J_(k, n - 1 - g) = fw[uc] ? xw[uc] * (t1 + n1) - t2 : t2;
+              carry = fw[uc] ? n1 : t1;
             }
           }
         }
@@ -1061,26 +1075,36 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, OCC)
       for (int k = kRegJ ? n : ls; k < n; k += S) {
         double carry = J_(k, qq);
         for (int gb = 0; gb < ng; gb += kU) {
-          double t2v[kU], cv[kU], sw[kU], xw[kU];
-          bool fw[kU];
+          constexpr int kUC = GJR ? 1 : kU;
+          double t2v[kU], cv[kUC], sw[kUC], xw[kUC];
+          bool fw[kUC];
 #pragma unroll
           for (int u = 0; u < kU; u++) {
             const int g = gb + u;
             const bool ok = g < ng;
             t2v[u] = ok ? J_(k, qq + g + 1) : 0.0;
-            cv[u] = ok ? gc[g] : 0.0;
-            sw[u] = ok ? gs[g] : 0.0;
-            xw[u] = ok ? gx[g] : 0.0;
-            fw[u] = ok && gf[g] != 0.0;
+            if constexpr (!GJR) {
+              cv[u] = ok ? gc[g] : 0.0;
+              sw[u] = ok ? gs[g] : 0.0;
+              xw[u] = ok ? gx[g] : 0.0;
+              fw[u] = ok && gf[g] != 0.0;
+            }
           }
 #pragma unroll
           for (int u = 0; u < kU; u++) {
             const int g = gb + u;
             if (g < ng) {
+              const int uc = GJR ? 0 : u;
+              if constexpr (GJR) {
+                cv[0] = gc[g];
+                sw[0] = gs[g];
+                xw[0] = gx[g];
+                fw[0] = gf[g] != 0.0;
+              }
               const double t1 = carry, t2 = t2v[u];
-              const double n1 = t1 * cv[u] + t2 * sw[u];
-              J_(k, qq + g) = fw[u] ? n1 : t1;
-              carry = fw[u] ? xw[u] * (n1 + t1) - t2 : t2;
+              const double n1 = t1 * cv[uc] + t2 * sw[uc];
+              J_(k, qq + g) = fw[uc] ? n1 : t1;
+              carry = fw[uc] ? xw[uc] * (n1 + t1) - t2 : t2;
             }
           }
         }
