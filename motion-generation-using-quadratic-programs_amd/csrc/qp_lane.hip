@@ -120,6 +120,12 @@ constexpr int kScanDepth = QPGPU_SCAN_DEPTH;
 #ifndef QPGPU_LANE_SCANG
 #define QPGPU_LANE_SCANG 1
 #endif
+// cache policy of the once-read LDS-DMA staging (G, g0, CE, ce0): 0 default, 2 non-temporal (so
+// the stream does not evict the CI lines the later l1 scans re-read from L2)
+#ifndef QPGPU_LANE_STAGE_NT
+#define QPGPU_LANE_STAGE_NT 0
+#endif
+constexpr int kStageAux = QPGPU_LANE_STAGE_NT ? 2 : 0;
 static_assert(kScanDepth >= 2, "the pipelined scan needs at least two row buffers");
 
 __device__ __forceinline__ bool wave_any(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
@@ -164,7 +170,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
       const int e = k + 2 * lane;
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(e < nd ? src + e : src),
-          (__attribute__((address_space(3))) void*)(sbuf + off + k), 16, 0, 0);
+          (__attribute__((address_space(3))) void*)(sbuf + off + k), 16, 0, kStageAux);
     }
   };
   // whole tile of X (E doubles per QP) -> sbuf[off...]

@@ -215,6 +215,9 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
 #ifndef QPGPU_WAVE_REGJ
 #define QPGPU_WAVE_REGJ 0
 #endif
+#ifndef QPGPU_WAVE_RPACK
+#define QPGPU_WAVE_RPACK 1
+#endif
 #ifndef QPGPU_WAVE_REGSETUP
 #define QPGPU_WAVE_REGSETUP 1
 #endif
@@ -257,11 +260,30 @@ struct WaveLay {
   int js, nr, off_r, off_sc, off_x, off_z, off_d, off_np, off_rv, off_xo, off_gc, off_u, off_uo, off_s,
       off_a, off_fl, off_ctl, stride;
 };
-__host__ __device__ inline WaveLay wave_lay(int n, int m, bool gjr, bool regj = false) {
+__host__ __device__ inline WaveLay wave_lay(int n, int m, bool gjr, bool regj = false, bool rpack = false) {
   WaveLay L;
   L.js = (n + 1) | 1;
   L.nr = n * (n + 1) / 2 + (n > 0 ? n - 1 : 0) + 1;
-  if (!regj) {
+  if (rpack && !regj && !gjr) {
+    // J [n][js] at 0, R packed after it, the loop's vectors, then x z d; during the setup the
+    // factor L ([n][js]) overlays R and the loop's vectors
+    L.off_r = n * L.js;
+    L.off_sc = L.off_r;
+    L.off_np = L.off_r + L.nr;
+    L.off_rv = L.off_np + n;
+    L.off_xo = L.off_rv + n;
+    L.off_gc = L.off_xo + n;
+    L.off_u = L.off_gc + 4 * n;
+    L.off_uo = L.off_u + n + 1;
+    L.off_s = L.off_uo + n + 1;
+    L.off_a = L.off_s + m;
+    L.off_fl = L.off_a + (2 * (n + 1) + 1) / 2;
+    const int end = L.off_fl + (2 * m + 7) / 8;
+    L.off_x = end > L.off_r + n * L.js ? end : L.off_r + n * L.js;
+    L.off_z = L.off_x + n;
+    L.off_d = L.off_z + n;
+    L.off_ctl = L.off_d + n;
+  } else if (!regj) {
     L.off_r = gjr ? 0 : n * L.js;
     L.off_sc = L.off_r;
     L.off_x = gjr ? 0 : 2 * n * L.js;
@@ -318,6 +340,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   constexpr bool kRegJ = QPGPU_WAVE_REGJ && !GJR && S <= 32 && NMAX <= S && OCC == 2;
   constexpr bool kRegSetup = QPGPU_WAVE_REGSETUP && !GJR && NMAX <= S &&
                              ((S == 32 && OCC == 1) || (S == 16 && OCC <= 2) || kRegJ);
+  // R packed (upper triangle + subdiagonal) with J still in LDS: less LDS per QP, more resident
+  // blocks per CU (the register setup keeps the factor L in its own overlay)
+  constexpr bool kRPack = QPGPU_WAVE_RPACK && kRegSetup && !kRegJ;
+  constexpr bool kPackedR = kRegJ || kRPack;
   // lane-parallel selections (argmin of s for l2, of u/r for t1) for one-wave subgroups
   constexpr bool kLaneSel = S <= 64;
   // the one-wave-per-SIMD variant keeps each lane's CI columns (and ci0) in registers from the
@@ -331,7 +357,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   // workspace variant, whose lanes have registers to spare)
   constexpr int KG = GJR ? 16 : kUG;
   extern __shared__ double lds[];
-  const WaveLay Ly = wave_lay(a.n, a.m, GJR, kRegJ);
+  const WaveLay Ly = wave_lay(a.n, a.m, GJR, kRegJ, kRPack);
   const int JS = GJR ? BigWs<NMAX>::JS : Ly.js;
 
   const int tid = threadIdx.x;
@@ -379,7 +405,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   // J in LDS: row-major.  J in the workspace (GJR): column-major, so that the row-parallel work
   // (Givens sweeps, update_z, building J) reads and writes it coalesced across lanes.
 #define J_(i, j) (GJR ? Jm[(j) * JS + (i)] : Jm[(i) * JS + (j)])
-#define R_(i, j) Rm[kRegJ ? rpk((i), (j), n) : (i) * JS + (j)]
+#define R_(i, j) Rm[kPackedR ? rpk((i), (j), n) : (i) * JS + (j)]
 #define L_(i, j) Lm[(i) * JS + (j)]
   // J in registers (kRegJ): lane r holds row r, indexed with compile-time column indices only
   [[maybe_unused]] double Jr[kRegJ ? NMAX : 1];
@@ -668,7 +694,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   }
   if (chol_ok) {
     // R = 0 (L no longer needed), flags
-    for (int e = ls; e < (kRegJ ? Ly.nr : n * JS); e += S) Rm[e] = 0.0;
+    for (int e = ls; e < (kPackedR ? Ly.nr : n * JS); e += S) Rm[e] = 0.0;
     for (int i = ls; i < m; i += S) act[i] = exc[i] = 0;
     for (int i = ls; i <= n; i += S) {
       uv[i] = 0.0;
@@ -1556,19 +1582,22 @@ static hipError_t launch_wave(const QpArgs& a, hipStream_t stream, double* ws) {
   // i.e. >= 8 one-wave blocks per CU) register pressure is the occupancy limit, so launch the
   // instantiation compiled for 4 waves per SIMD (a few spilled VGPRs).  Measured: mgqp level 0
   // (10.5 KiB per block) 2.44 -> 2.32 ms; C3 (37 KiB per block, LDS-limited to one wave per SIMD)
-  // keeps the unconstrained allocation (21.0 vs 22.0 ms).
+  // keeps the unconstrained allocation (21.0 vs 22.0 ms).  The register-setup instantiations
+  // (OCC 2 for S = 16, OCC 1) use the packed-R layout when QPGPU_WAVE_RPACK is on.
   if constexpr (S < 64 && !GJR) {
     if (lds_bytes <= 20480) {
       hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR, 4>), dim3((unsigned)blocks), dim3(C::BS),
                          lds_bytes, stream, a, ws);
       return hipGetLastError();
     }
+    const size_t lds_p = (size_t)C::QPB * wave_lay(a.n, a.m, GJR, false, QPGPU_WAVE_RPACK != 0).stride * sizeof(double);
     // four-QP waves (S = 16): up to 40 KiB per block still leaves room for two waves per SIMD
     if (S == 16 && lds_bytes <= 40960) {
       hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR, 2>), dim3((unsigned)blocks), dim3(C::BS),
-                         lds_bytes, stream, a, ws);
+                         lds_p, stream, a, ws);
       return hipGetLastError();
     }
+    lds_bytes = lds_p;  // OCC 1 (register setup) from here on
   }
   // workspace variant (n > 64): QPGPU_WAVE_GJR_BLOCKS_PER_CU = k pads the dynamic LDS so at most
   // k one-QP workgroups share a CU (diagnostic: fewer resident QPs = a working set that stays in

@@ -96,6 +96,16 @@ for s in $STEPS; do
     c5res)
       # C5 with the number of resident QPs per CU capped (Infinity-Cache residency experiment)
       for k in ${CAPS:-1 2 4}; do QPGPU_WAVE_GJR_BLOCKS_PER_CU=$k run bench_C5_cap$k 600 python bench.py --config C5 --no-cpu --steps 2 --warmup 1 --kernel-reps 2; done ;;
+    abpmc)
+      # FETCH_SIZE of the C1 kernel for the in-tree build and each A/B variant (one pass each)
+      run pmcab_base 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcab_base" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --streams 1
+      for v in ${VARIANTS}; do QPGPU_LIB_PATH=_ab/$v/libqpgpu.so run pmcab_$v 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcab_$v" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --streams 1; done
+      for d in "$OUT"/pmcab_*/; do python3 - "$d" <<'PY'
+import csv, statistics, sys
+vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(sys.argv[1] + "c1_counter_collection.csv")) if "qp_lane" in r["Kernel_Name"]]
+print(sys.argv[1], "FETCH_SIZE KiB median", statistics.median(vals), "-> bytes x2", 2 * 1024 * statistics.median(vals))
+PY
+      done ;;
     listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;
     sq)
       for f in ${FAMILIES:-lane subgroup}; do
