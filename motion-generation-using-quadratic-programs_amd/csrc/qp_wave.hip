@@ -773,9 +773,11 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
     if constexpr (!GJR) {
       if (lead)
         for (int i = iq - 1; i >= 0; i--) {
-          const double s = seq_fma_up<kUL>(0.0, i + 1, iq, [&](int j) { return R_(i, j); },
+          // row i of R as a pointer (Ri[j] = R[i][j], j >= i): packed rows are contiguous too
+          const double* Ri = kPackedR ? Rm + (i * n - (i * (i - 1)) / 2 - i) : Rm + i * JS;
+          const double s = seq_fma_up<kUL>(0.0, i + 1, iq, [&](int j) { return Ri[j]; },
                                       [&](int j) { return rv[j]; });
-          rv[i] = (dv[i] - s) / R_(i, i);
+          rv[i] = (dv[i] - s) / Ri[i];
         }
     } else {
       if (ls >= 64) return;  // waves 1.. idle (they wait at the caller's grp_sync)
