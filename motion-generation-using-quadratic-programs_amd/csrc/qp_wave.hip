@@ -1308,6 +1308,55 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
             exc[i] = 0;
           }
         }
+      } else if constexpr (!GJR && MMAX <= 2 * S) {
+        // a lane's two constraints (i0 = ls, i1 = ls + S) summed together, so each chunk of CI
+        // loads covers both and a scan waits on half as many memory latencies; each sum keeps the
+        // reference's j order (the second constraint's index is clamped when it does not exist,
+        // its sum then discarded)
+        const int i0 = ls, i1 = ls + S;
+        const bool h0 = i0 < m, h1 = i1 < m;
+        const int c0i = h0 ? i0 : 0, c1i = h1 ? i1 : c0i;
+        const double c00 = EL(ci0b, c0i), c01 = EL(ci0b, c1i);
+        double s0 = 0.0, s1 = 0.0;
+        int jb = 0;
+        for (; jb + KG <= n; jb += KG) {
+          double a0[KG], a1[KG], xw[KG];
+#pragma unroll
+          for (int u = 0; u < KG; u++) {
+            a0[u] = EL(CIb, (jb + u) * m + c0i);
+            a1[u] = EL(CIb, (jb + u) * m + c1i);
+            xw[u] = xv[jb + u];
+          }
+#pragma unroll
+          for (int u = 0; u < KG; u++) {
+            s0 += a0[u] * xw[u];
+            s1 += a1[u] * xw[u];
+          }
+        }
+        if (jb < n) {
+          double a0[KG], a1[KG], xw[KG];
+#pragma unroll
+          for (int u = 0; u < KG; u++) {
+            const int jj = jb + u < n ? jb + u : n - 1;
+            a0[u] = EL(CIb, jj * m + c0i);
+            a1[u] = EL(CIb, jj * m + c1i);
+            xw[u] = xv[jj];
+          }
+#pragma unroll
+          for (int u = 0; u < KG; u++)
+            if (jb + u < n) {
+              s0 += a0[u] * xw[u];
+              s1 += a1[u] * xw[u];
+            }
+        }
+        if (h0) {
+          sv[i0] = s0 + c00;
+          exc[i0] = 0;
+        }
+        if (h1) {
+          sv[i1] = s1 + c01;
+          exc[i1] = 0;
+        }
       } else {
         for (int i = ls; i < m; i += S) {
           const double c0 = EL(ci0b, i);  // issued with the first chunk, added last
