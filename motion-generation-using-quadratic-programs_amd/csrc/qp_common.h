@@ -31,6 +31,35 @@ __device__ __forceinline__ double qp_distance(double a, double b) {
   return (gt || lt) ? h : a1 * kSqrt2;
 }
 
+// sqrt(x) for x in [1, 2] (or NaN): the compiler's correctly rounded binary64 sqrt sequence
+// (v_rsq_f64 seed, Goldschmidt / Newton refinement) without its range scaling (an ldexp by 0
+// for x >= 2^-767) and its +-0 / +inf pass-through, neither of which can apply on [1, 2] —
+// the same bits in ~8 fewer instructions.  tools/sqrt_probe.hip checks it against sqrt() over
+// the whole interval.
+__device__ __forceinline__ double sqrt_1to2(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  return __builtin_fma(d, h, g);
+}
+
+// distance() with sqrt_1to2: 1 + t*t lies in [1, 2] whenever the selected branch uses it
+// (t = num / den with num <= den; the equal-magnitude branch discards it)
+__device__ __forceinline__ double qp_distance_f(double a, double b) {
+  const double a1 = fabs(a), b1 = fabs(b);
+  const bool gt = a1 > b1, lt = b1 > a1;
+  const double num = gt ? b1 : a1;
+  const double den = gt ? a1 : b1;
+  const double t = num / den;
+  const double h = den * sqrt_1to2(1.0 + t * t);
+  return (gt || lt) ? h : a1 * kSqrt2;
+}
+
 // Ordering point for LDS hand-offs between lanes of ONE wavefront.  A QP is always owned by
 // lanes of a single wave that are converged with each other (every control decision is a
 // function of replicated values), and a wave's LDS instructions execute in issue order, so a

@@ -221,6 +221,27 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
 #ifndef QPGPU_WAVE_REGSETUP
 #define QPGPU_WAVE_REGSETUP 1
 #endif
+// update_r on the lead with row i-1's row values and first chunk of its R and r entries loaded
+// while row i's division is in flight, r[i+1] carried in a register, later chunks double-buffered
+#ifndef QPGPU_WAVE_URPF
+#define QPGPU_WAVE_URPF 1
+#endif
+#ifndef QPGPU_WAVE_URU
+#define QPGPU_WAVE_URU 4
+#endif
+// add_constraint's |h| chain in unmasked chunks + a one-rotation tail, qp_distance_f
+#ifndef QPGPU_WAVE_HCHAIN2
+#define QPGPU_WAVE_HCHAIN2 1
+#endif
+// CI loads per chunk of the two-constraint l1 scan (one global-memory round trip per chunk)
+#ifndef QPGPU_WAVE_SCANKG
+#define QPGPU_WAVE_SCANKG 8
+#endif
+// diagnostic stamps only: slots 5..7 hold the loop's update_r cycles, step count and sum of iq
+// over steps instead of the equality-phase parts
+#ifndef QPGPU_WAVE_STAMPS_DETAIL
+#define QPGPU_WAVE_STAMPS_DETAIL 0
+#endif
 // per-QP control block (lead lane writes, subgroup reads after grp_sync)
 struct Ctl {
   double f, t, t1, t2, ss, R_norm, c1, c2, psi, ci0ip, znp;
@@ -708,7 +729,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   // d = J^T np (lane = column, j ascending); z = J[:, iq:] d[iq:] (lane = row)
   // diagnostic clocks (stamps only): loop phases (scan, select, d/z, lead step, add, delete) and
   // equality-phase parts (d/z, update_r, lead t2 + x/u, add_constraint, the lead's |h| chains)
-  uint64_t tph[6] = {0, 0, 0, 0, 0, 0}, teq[5] = {0, 0, 0, 0, 0};
+  uint64_t tph[6] = {0, 0, 0, 0, 0, 0}, teq[5] = {0, 0, 0, 0, 0}, tdet[3] = {0, 0, 0};
   auto clk = [&]() -> uint64_t { return a.stamps ? __builtin_amdgcn_s_memtime() : 0; };
   auto compute_d_z = [&](int iq) {
     if constexpr (kRegJ) {
@@ -770,7 +791,75 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   // as the reference's `R[i][j] * r[j]`) to LDS; the lead then adds them in j order.  Called by
   // every lane of the subgroup.
   auto update_r = [&](int iq) {
-    if constexpr (!GJR) {
+    if constexpr (!GJR && QPGPU_WAVE_URPF) {
+      // row i: s = R[i][i+1] r[i+1] + sum_{j >= i+2} R[i][j] r[j] in j order (the reference's
+      // order: +0.0 first, then each product).  r[i+1] stays in a register (no LDS round trip on
+      // the chain); the next row's loads (R[i-1][i-1..i+U], d[i-1], r[i+1..i+U]) are
+      // unconditional (no exec-mask branch per load) and follow row i's division, before r[i]
+      // is stored (issuing them ahead of row i's chain instead measured no faster).  Entries
+      // past the row are read (in-bounds LDS, any value) and their products replaced by +0.0:
+      // s is never -0.0 (it starts at +0.0 and a sum is -0.0 only from two -0.0 operands), so
+      // adding +0.0 leaves it unchanged.
+      if (lead && iq > 0) {
+        constexpr int U = QPGPU_WAVE_URU;
+        auto rowp = [&](int i) -> const double* {
+          return kPackedR ? Rm + (i * n - (i * (i - 1)) / 2 - i) : Rm + i * JS;
+        };
+        double nd, nRii, nR1, nR[U], nr[U];  // the next row's values
+        auto prefetch = [&](int i) {
+          const double* Ri = rowp(i);
+          nd = dv[i];
+          nRii = Ri[i];
+          nR1 = Ri[i + 1];
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            nR[u] = Ri[i + 2 + u];
+            nr[u] = rv[i + 2 + u];
+          }
+        };
+        prefetch(iq - 1);
+        double rn = 0.0;  // r[i+1]
+        for (int i = iq - 1; i >= 0; i--) {
+          const double di = nd, Rii = nRii, R1 = nR1;
+          double cR[U], cr[U];
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            cR[u] = nR[u];
+            cr[u] = nr[u];
+          }
+          const double p1 = i + 1 < iq ? R1 * rn : 0.0;
+          double s = 0.0;
+          s += p1;
+          const int c = iq - (i + 2);  // valid entries of the chunk
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            const double q = cR[u] * cr[u];
+            s += u < c ? q : 0.0;
+          }
+          if (c > U) {
+            const double* Ri = rowp(i);
+            for (int jb = i + 2 + U; jb < iq; jb += U) {
+              double aR[U], ar[U];
+#pragma unroll
+              for (int u = 0; u < U; u++) {
+                aR[u] = Ri[jb + u];
+                ar[u] = rv[jb + u];
+              }
+              const int cc = iq - jb;
+#pragma unroll
+              for (int u = 0; u < U; u++) {
+                const double q = aR[u] * ar[u];
+                s += u < cc ? q : 0.0;
+              }
+            }
+          }
+          const double r = (di - s) / Rii;
+          prefetch(i > 0 ? i - 1 : 0);  // r[i+1 ..] are in LDS already; r[i] is carried
+          rv[i] = r;
+          rn = r;
+        }
+      }
+    } else if constexpr (!GJR) {
       if (lead)
         for (int i = iq - 1; i >= 0; i--) {
           // row i of R as a pointer (Ri[j] = R[i][j], j >= i): packed rows are contiguous too
@@ -860,7 +949,38 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
     if (lead) {
       const int iq = ctl->iq;
       int ng = 0;
-      if (iq < n) {
+      if (QPGPU_WAVE_HCHAIN2 && iq < n) {
+        // full chunks of U rotations without per-rotation exec-mask branches (the chunk's d
+        // values loaded together), then the tail one rotation per trip; distance() with the
+        // range-reduced sqrt (qp_common.h, same bits)
+        double carried = dv[n - 1];
+        constexpr int U = 4;
+        int jb = n - 1;
+        for (; jb - U >= iq; jb -= U) {
+          double ac[U];
+#pragma unroll
+          for (int u = 0; u < U; u++) ac[u] = dv[jb - u - 1];
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            const double a0 = ac[u];
+            const double h = qp_distance_f(a0, carried);
+            const bool skip = fabs(h) < kEps;
+            gf[ng + u] = skip ? 0.0 : 1.0;
+            gx[ng + u] = h;
+            carried = skip ? a0 : h;
+          }
+          ng += U;
+        }
+        for (; jb >= iq + 1; jb--) {
+          const double a0 = dv[jb - 1];
+          const double h = qp_distance_f(a0, carried);
+          const bool skip = fabs(h) < kEps;
+          gf[ng] = skip ? 0.0 : 1.0;
+          gx[ng] = h;
+          carried = skip ? a0 : h;
+          ng++;
+        }
+      } else if (iq < n) {
         double carried = dv[n - 1];
         constexpr int U = 8;  // d values of a chunk loaded together, ahead of the h chain
         for (int jb = n - 1; jb >= iq + 1; jb -= U) {
@@ -1317,33 +1437,34 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         const bool h0 = i0 < m, h1 = i1 < m;
         const int c0i = h0 ? i0 : 0, c1i = h1 ? i1 : c0i;
         const double c00 = EL(ci0b, c0i), c01 = EL(ci0b, c1i);
+        constexpr int SKG = QPGPU_WAVE_SCANKG;
         double s0 = 0.0, s1 = 0.0;
         int jb = 0;
-        for (; jb + KG <= n; jb += KG) {
-          double a0[KG], a1[KG], xw[KG];
+        for (; jb + SKG <= n; jb += SKG) {
+          double a0[SKG], a1[SKG], xw[SKG];
 #pragma unroll
-          for (int u = 0; u < KG; u++) {
+          for (int u = 0; u < SKG; u++) {
             a0[u] = EL(CIb, (jb + u) * m + c0i);
             a1[u] = EL(CIb, (jb + u) * m + c1i);
             xw[u] = xv[jb + u];
           }
 #pragma unroll
-          for (int u = 0; u < KG; u++) {
+          for (int u = 0; u < SKG; u++) {
             s0 += a0[u] * xw[u];
             s1 += a1[u] * xw[u];
           }
         }
         if (jb < n) {
-          double a0[KG], a1[KG], xw[KG];
+          double a0[SKG], a1[SKG], xw[SKG];
 #pragma unroll
-          for (int u = 0; u < KG; u++) {
+          for (int u = 0; u < SKG; u++) {
             const int jj = jb + u < n ? jb + u : n - 1;
             a0[u] = EL(CIb, jj * m + c0i);
             a1[u] = EL(CIb, jj * m + c1i);
             xw[u] = xv[jj];
           }
 #pragma unroll
-          for (int u = 0; u < KG; u++)
+          for (int u = 0; u < SKG; u++)
             if (jb + u < n) {
               s0 += a0[u] * xw[u];
               s1 += a1[u] * xw[u];
@@ -1462,7 +1583,12 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
     uint64_t t1c = clk();
     tph[2] += t1c - t0;
     int kind = 0;  // 1 infeasible, 2 dual step, 3 full step, 4 partial step
+    if (QPGPU_WAVE_STAMPS_DETAIL) {
+      tdet[1] += 1;
+      tdet[2] += ctl->iq;
+    }
     update_r(ctl->iq);
+    if (QPGPU_WAVE_STAMPS_DETAIL) tdet[0] += clk() - t1c;
     // t1 = min over active inequalities with r > 0 of u/r (first index on ties), l its constraint
     [[maybe_unused]] double t1best = inf;
     [[maybe_unused]] int kbest = INT_MAX;
@@ -1596,7 +1722,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   if (a.stamps && threadIdx.x == 0)
     for (int k = 0; k < 6; k++) a.stamps[(uint64_t)blockIdx.x * kStampSlots + 8 + k] = tph[k];
   if (a.stamps && threadIdx.x == 0) {
-    for (int k = 0; k < 3; k++) a.stamps[(uint64_t)blockIdx.x * kStampSlots + 5 + k] = teq[k];
+    for (int k = 0; k < 3; k++)
+      a.stamps[(uint64_t)blockIdx.x * kStampSlots + 5 + k] = QPGPU_WAVE_STAMPS_DETAIL ? tdet[k] : teq[k];
     for (int k = 3; k < 5; k++) a.stamps[(uint64_t)blockIdx.x * kStampSlots + 11 + k] = teq[k];
   }
   // ------------------------------------------------------------------ outputs

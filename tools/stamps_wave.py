@@ -37,7 +37,9 @@ for k, nm in enumerate(names):
     print(f"  {nm:15s} mean {d.mean():10.0f} p50 {np.median(d):10.0f} max {d.max():10d}")
 for k, nm in enumerate(["scan", "select", "d/z", "lead step", "add_constraint", "delete"]):
     print(f"    loop {nm:15s} mean {s[:, 8 + k].mean():10.0f}")
-for k, nm in [(5, "eq d/z"), (6, "eq update_r"), (7, "eq lead t2 + x/u"), (14, "eq add_constraint"),
+det = os.environ.get("WDETAIL") == "1"  # a QPGPU_WAVE_STAMPS_DETAIL=1 build
+for k, nm in [(5, "loop update_r" if det else "eq d/z"), (6, "loop steps" if det else "eq update_r"),
+              (7, "loop sum iq" if det else "eq lead t2 + x/u"), (14, "eq add_constraint"),
               (15, "|h| chains (eq + loop)")]:
     print(f"    {nm:20s} mean {s[:, k].mean():10.0f}")
 it = db.iters.cpu().numpy()
