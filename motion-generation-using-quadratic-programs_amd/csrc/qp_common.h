@@ -18,19 +18,6 @@ constexpr double kSqrt2 = 1.4142135623730951;         // sqrt(2.0), .rodata +0x1
 
 __device__ __forceinline__ double dinf() { return __builtin_inf(); }
 
-// distance(a, b) — the reference's overflow-safe hypot (three branches), evaluated branch-free
-// so that divergent lanes do not serialise; the selected branch computes exactly the same
-// operations as the reference's.
-__device__ __forceinline__ double qp_distance(double a, double b) {
-  const double a1 = fabs(a), b1 = fabs(b);
-  const bool gt = a1 > b1, lt = b1 > a1;
-  const double num = gt ? b1 : a1;
-  const double den = gt ? a1 : b1;
-  const double t = num / den;
-  const double h = den * sqrt(1.0 + t * t);
-  return (gt || lt) ? h : a1 * kSqrt2;
-}
-
 // sqrt(x) for x in [1, 2] (or NaN): the compiler's correctly rounded binary64 sqrt sequence
 // (v_rsq_f64 seed, Goldschmidt / Newton refinement) without its range scaling (an ldexp by 0
 // for x >= 2^-767) and its +-0 / +inf pass-through, neither of which can apply on [1, 2] —
@@ -48,15 +35,28 @@ __device__ __forceinline__ double sqrt_1to2(double x) {
   return __builtin_fma(d, h, g);
 }
 
-// distance() with sqrt_1to2: 1 + t*t lies in [1, 2] whenever the selected branch uses it
-// (t = num / den with num <= den; the equal-magnitude branch discards it)
-__device__ __forceinline__ double qp_distance_f(double a, double b) {
+// distance(a, b) — the reference's overflow-safe hypot (three branches), evaluated branch-free
+// so that divergent lanes do not serialise; the selected branch computes exactly the same
+// operations as the reference's.  1 + t*t lies in [1, 2] whenever the selected branch uses it
+// (t = num / den with num <= den; the equal-magnitude branch discards it): sqrt_1to2.
+__device__ __forceinline__ double qp_distance(double a, double b) {
   const double a1 = fabs(a), b1 = fabs(b);
   const bool gt = a1 > b1, lt = b1 > a1;
   const double num = gt ? b1 : a1;
   const double den = gt ? a1 : b1;
   const double t = num / den;
   const double h = den * sqrt_1to2(1.0 + t * t);
+  return (gt || lt) ? h : a1 * kSqrt2;
+}
+
+// the same with the library sqrt() (tools/sqrt_probe.hip checks the two against each other)
+__device__ __forceinline__ double qp_distance_libm(double a, double b) {
+  const double a1 = fabs(a), b1 = fabs(b);
+  const bool gt = a1 > b1, lt = b1 > a1;
+  const double num = gt ? b1 : a1;
+  const double den = gt ? a1 : b1;
+  const double t = num / den;
+  const double h = den * sqrt(1.0 + t * t);
   return (gt || lt) ? h : a1 * kSqrt2;
 }
 

@@ -952,7 +952,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       if (QPGPU_WAVE_HCHAIN2 && iq < n) {
         // full chunks of U rotations without per-rotation exec-mask branches (the chunk's d
         // values loaded together), then the tail one rotation per trip; distance() with the
-        // range-reduced sqrt (qp_common.h, same bits)
+        // range-reduced sqrt (qp_common.h)
         double carried = dv[n - 1];
         constexpr int U = 4;
         int jb = n - 1;
@@ -963,7 +963,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
 #pragma unroll
           for (int u = 0; u < U; u++) {
             const double a0 = ac[u];
-            const double h = qp_distance_f(a0, carried);
+            const double h = qp_distance(a0, carried);
             const bool skip = fabs(h) < kEps;
             gf[ng + u] = skip ? 0.0 : 1.0;
             gx[ng + u] = h;
@@ -973,7 +973,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         }
         for (; jb >= iq + 1; jb--) {
           const double a0 = dv[jb - 1];
-          const double h = qp_distance_f(a0, carried);
+          const double h = qp_distance(a0, carried);
           const bool skip = fabs(h) < kEps;
           gf[ng] = skip ? 0.0 : 1.0;
           gx[ng] = h;

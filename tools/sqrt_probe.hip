@@ -1,6 +1,6 @@
 // sqrt_probe.hip — diagnostic (not part of the product): checks qpk::sqrt_1to2 against the
 // compiler's sqrt() bit for bit on the GPU, for every x in [1, 2) on a stride of binary64
-// patterns (plus both ends and random mantissas), and qp_distance_f against qp_distance on
+// patterns (plus both ends and random mantissas), and qp_distance (sqrt_1to2) against qp_distance_libm (sqrt()) on
 // random operand pairs including zeros, equal magnitudes, infinities, NaN and denormals.
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o tools/sqrt_probe tools/sqrt_probe.hip
 #include <hip/hip_runtime.h>
@@ -45,7 +45,7 @@ __global__ void dist_kernel(unsigned long long* bad, unsigned long long n) {
   h2 ^= h2 >> 31;
   const double a = pick(h1);
   const double b = (i % 5 == 0) ? -a : pick(h2);
-  const double r1 = qpk::qp_distance(a, b), r2 = qpk::qp_distance_f(a, b);
+  const double r1 = qpk::qp_distance_libm(a, b), r2 = qpk::qp_distance(a, b);
   const bool n1 = r1 != r1, n2 = r2 != r2;
   if (n1 != n2 || (!n1 && __builtin_bit_cast(unsigned long long, r1) != __builtin_bit_cast(unsigned long long, r2)))
     atomicAdd(bad, 1ull);
@@ -62,6 +62,6 @@ int main() {
   unsigned long long h[2];
   hipMemcpy(h, bad, 16, hipMemcpyDeviceToHost);
   printf("sqrt_1to2 vs sqrt: %llu mismatches of %llu\n", h[0], n);
-  printf("qp_distance_f vs qp_distance: %llu mismatches of %llu\n", h[1], nd);
+  printf("qp_distance vs qp_distance_libm: %llu mismatches of %llu\n", h[1], nd);
   return (h[0] || h[1]) ? 1 : 0;
 }
