@@ -78,6 +78,41 @@ __device__ __forceinline__ double seq_fma_up(double s, int j0, int j1, FA A, FB 
   return s;
 }
 
+// seq_fma_up for operands in LDS with s starting at +0.0: the partial chunk's loads are
+// unconditional (past j1 they read whatever lies there — in-bounds LDS) and its products past
+// j1 are replaced by +0.0, so there is no exec-mask branch per load.  A sum that starts at
+// +0.0 is never -0.0 (a sum is -0.0 only from two -0.0 operands), so adding +0.0 leaves it
+// unchanged.
+template <int kU, class FA, class FB>
+__device__ __forceinline__ double seq_fma_up_lds(double s, int j0, int j1, FA A, FB B) {
+  int jb = j0;
+  for (; jb + kU <= j1; jb += kU) {
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      va[u] = A(jb + u);
+      vb[u] = B(jb + u);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) s += va[u] * vb[u];
+  }
+  if (jb < j1) {
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      va[u] = A(jb + u);
+      vb[u] = B(jb + u);
+    }
+    const int c = j1 - jb;
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const double q = va[u] * vb[u];
+      s += u < c ? q : 0.0;
+    }
+  }
+  return s;
+}
+
 // s - sum A(j) * B(j), j ascending (s -= a*b per element)
 template <int kU, class FA, class FB>
 __device__ __forceinline__ double seq_fms_up(double s, int j0, int j1, FA A, FB B) {
@@ -777,10 +812,12 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       grp_sync<S>();
     } else {
       for (int c = ls; c < n; c += S)
-        dv[c] = seq_fma_up<GJR ? KG : kUL>(0.0, 0, n, [&](int j) { return J_(j, c); }, [&](int j) { return npv[j]; });
+        dv[c] = GJR ? seq_fma_up<KG>(0.0, 0, n, [&](int j) { return J_(j, c); }, [&](int j) { return npv[j]; })
+                    : seq_fma_up_lds<kUL>(0.0, 0, n, [&](int j) { return J_(j, c); }, [&](int j) { return npv[j]; });
       grp_sync<S>();
       for (int r = ls; r < n; r += S)
-        zv[r] = seq_fma_up<GJR ? KG : kUL>(0.0, iq, n, [&](int j) { return J_(r, j); }, [&](int j) { return dv[j]; });
+        zv[r] = GJR ? seq_fma_up<KG>(0.0, iq, n, [&](int j) { return J_(r, j); }, [&](int j) { return dv[j]; })
+                    : seq_fma_up_lds<kUL>(0.0, iq, n, [&](int j) { return J_(r, j); }, [&](int j) { return dv[j]; });
       grp_sync<S>();
     }
   };
@@ -912,25 +949,28 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   auto dot2_lead = [&](double& zz, double& znp) {
     double s1 = 0.0, s2 = 0.0;
     constexpr int U = 8;  // loads of a chunk issued together (the adds stay in i order)
+    // loads unconditional (in-bounds LDS past n), products past n replaced by +0.0: both sums
+    // start at +0.0, so they are never -0.0 and adding +0.0 leaves them unchanged
     for (int ib = 0; ib < n; ib += U) {
       double zc[U], pc[U];
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        zc[u] = ib + u < n ? zv[ib + u] : 0.0;
-        pc[u] = ib + u < n ? npv[ib + u] : 0.0;
+        zc[u] = zv[ib + u];
+        pc[u] = npv[ib + u];
       }
+      const int c = n - ib;
 #pragma unroll
-      for (int u = 0; u < U; u++)
-        if (ib + u < n) {
-          s1 += zc[u] * zc[u];
-          s2 += zc[u] * pc[u];
-        }
+      for (int u = 0; u < U; u++) {
+        const double q1 = zc[u] * zc[u], q2 = zc[u] * pc[u];
+        s1 += u < c ? q1 : 0.0;
+        s2 += u < c ? q2 : 0.0;
+      }
     }
     zz = s1;
     znp = s2;
   };
   auto dot_lead = [&](const double* u_, const double* v_) {
-    return seq_fma_up<8>(0.0, 0, n, [&](int i) { return u_[i]; }, [&](int i) { return v_[i]; });
+    return seq_fma_up_lds<8>(0.0, 0, n, [&](int i) { return u_[i]; }, [&](int i) { return v_[i]; });
   };
   // add_constraint (@.text+0x21fd), split in three:
   //  1. the lead runs the serial part of the d-chain.  Rotation g (j = n-1-g) computes
@@ -1495,10 +1535,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         for (int ib = 0; ib < m; ib += U) {
           double sc[U];
 #pragma unroll
-          for (int u = 0; u < U; u++) sc[u] = ib + u < m ? sv[ib + u] : 0.0;
+          for (int u = 0; u < U; u++) sc[u] = sv[ib + u];  // past m: in-bounds LDS, masked
+          const int c = m - ib;
 #pragma unroll
-          for (int u = 0; u < U; u++)
-            if (ib + u < m) psi += (sc[u] < 0.0) ? sc[u] : 0.0;
+          for (int u = 0; u < U; u++) psi += (u < c && sc[u] < 0.0) ? sc[u] : 0.0;
         }
         ctl->ss = 0.0;
         ctl->ip = 0;
@@ -1708,7 +1748,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       tph[5] += clk() - td;
     }
     if (lead) {
-      const double s = seq_fma_up<8>(0.0, 0, n, [&](int k) { return npv[k]; },
+      const double s = seq_fma_up_lds<8>(0.0, 0, n, [&](int k) { return npv[k]; },
                                 [&](int k) { return xv[k]; });
       sv[ctl->ip] = s + ctl->ci0ip;
       ctl->phase = PH_STEP;
