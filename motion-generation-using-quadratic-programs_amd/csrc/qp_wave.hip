@@ -268,12 +268,17 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
 #ifndef QPGPU_WAVE_HCHAIN2
 #define QPGPU_WAVE_HCHAIN2 1
 #endif
+// add_constraint's J sweep (J in LDS) in unmasked chunks + a one-rotation tail
+#ifndef QPGPU_WAVE_SWEEP2
+#define QPGPU_WAVE_SWEEP2 1
+#endif
 // CI loads per chunk of the two-constraint l1 scan (one global-memory round trip per chunk)
 #ifndef QPGPU_WAVE_SCANKG
 #define QPGPU_WAVE_SCANKG 8
 #endif
-// diagnostic stamps only: slots 5..7 hold the loop's update_r cycles, step count and sum of iq
-// over steps instead of the equality-phase parts
+// diagnostic stamps only: slots 5..7 hold, instead of the equality-phase parts, the loop's
+// update_r cycles, step count and sum of iq over steps (1), or add_constraint's |h| chain +
+// coefficients, J sweep and R column + test cycles, equality phase and loop together (2)
 #ifndef QPGPU_WAVE_STAMPS_DETAIL
 #define QPGPU_WAVE_STAMPS_DETAIL 0
 #endif
@@ -1079,6 +1084,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       }
     }
     grp_sync<S>();
+    const uint64_t h1 = clk();
+    if (QPGPU_WAVE_STAMPS_DETAIL == 2) tdet[0] += h1 - h0;
     const int iq0 = ctl->iq;
     if (kRegJ && iq0 < n) {
       // the same sweep on lane k's register row: rotation g = n-1-j on columns (j-1, j), j from
@@ -1097,6 +1104,44 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           Jr[j] = f ? xn * (t1 + n1) - t2 : t2;
           if (j % 4 == 0) __builtin_amdgcn_sched_barrier(0);  // coefficients 4 steps at a time
         }
+      }
+    } else if (!GJR && QPGPU_WAVE_SWEEP2 && iq0 < n) {
+      // the sweep below with J in LDS: full chunks of kU rotations with no per-rotation
+      // exec-mask branch (the chunk's J entries and coefficients loaded first), then the tail
+      // one rotation per trip
+      constexpr int kU = QPGPU_WAVE_KUJ;
+      const int ng = ctl->ngiv;
+      for (int k = ls; k < n; k += S) {
+        double carry = J_(k, n - 1);
+        int g = 0;
+        for (; g + kU <= ng; g += kU) {
+          double t1v[kU], cv[kU], sw[kU], xw[kU];
+          bool fw[kU];
+#pragma unroll
+          for (int u = 0; u < kU; u++) {
+            t1v[u] = J_(k, n - 2 - g - u);
+            cv[u] = gc[g + u];
+            sw[u] = gs[g + u];
+            xw[u] = gx[g + u];
+            fw[u] = gf[g + u] != 0.0;
+          }
+#pragma unroll
+          for (int u = 0; u < kU; u++) {
+            const double t1 = t1v[u], t2 = carry;
+            const double n1 = t1 * cv[u] + t2 * sw[u];
+            J_(k, n - 1 - g - u) = fw[u] ? xw[u] * (t1 + n1) - t2 : t2;
+            carry = fw[u] ? n1 : t1;
+          }
+        }
+        for (; g < ng; g++) {
+          const double t1 = J_(k, n - 2 - g), t2 = carry;
+          const double c = gc[g], sn = gs[g], xn = gx[g];
+          const bool f = gf[g] != 0.0;
+          const double n1 = t1 * c + t2 * sn;
+          J_(k, n - 1 - g) = f ? xn * (t1 + n1) - t2 : t2;
+          carry = f ? n1 : t1;
+        }
+        J_(k, n - 1 - ng) = carry;
       }
     } else if (iq0 < n) {
       // Row k's sweep over columns n-1 .. iq: rotation g maps (J[k][j-1], J[k][j]), j = n-1-g,
@@ -1148,6 +1193,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       }
     }
     grp_sync<S>();
+    const uint64_t h2 = clk();
+    if (QPGPU_WAVE_STAMPS_DETAIL == 2) tdet[1] += h2 - h1;
     if (iq0 < n)  // R[:iq+1, iq] = d[:iq+1], one entry per lane
       for (int i = ls; i <= iq0; i += S) R_(i, iq0) = dv[i];
     if (lead) {
@@ -1167,6 +1214,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       }
     }
     grp_sync<S>();
+    if (QPGPU_WAVE_STAMPS_DETAIL == 2) tdet[2] += clk() - h2;
   };
   // delete_constraint (@.text+0x26a8) of constraint l: the lead does the bookkeeping and the
   // R re-triangularisation (recording the rotations), the lanes shift R's rows and rotate
@@ -1623,12 +1671,12 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
     uint64_t t1c = clk();
     tph[2] += t1c - t0;
     int kind = 0;  // 1 infeasible, 2 dual step, 3 full step, 4 partial step
-    if (QPGPU_WAVE_STAMPS_DETAIL) {
+    if (QPGPU_WAVE_STAMPS_DETAIL == 1) {
       tdet[1] += 1;
       tdet[2] += ctl->iq;
     }
     update_r(ctl->iq);
-    if (QPGPU_WAVE_STAMPS_DETAIL) tdet[0] += clk() - t1c;
+    if (QPGPU_WAVE_STAMPS_DETAIL == 1) tdet[0] += clk() - t1c;
     // t1 = min over active inequalities with r > 0 of u/r (first index on ties), l its constraint
     [[maybe_unused]] double t1best = inf;
     [[maybe_unused]] int kbest = INT_MAX;

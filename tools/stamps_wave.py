@@ -37,9 +37,11 @@ for k, nm in enumerate(names):
     print(f"  {nm:15s} mean {d.mean():10.0f} p50 {np.median(d):10.0f} max {d.max():10d}")
 for k, nm in enumerate(["scan", "select", "d/z", "lead step", "add_constraint", "delete"]):
     print(f"    loop {nm:15s} mean {s[:, 8 + k].mean():10.0f}")
-det = os.environ.get("WDETAIL") == "1"  # a QPGPU_WAVE_STAMPS_DETAIL=1 build
-for k, nm in [(5, "loop update_r" if det else "eq d/z"), (6, "loop steps" if det else "eq update_r"),
-              (7, "loop sum iq" if det else "eq lead t2 + x/u"), (14, "eq add_constraint"),
+det = os.environ.get("WDETAIL", "0")  # the QPGPU_WAVE_STAMPS_DETAIL of the build
+lab = {"0": ["eq d/z", "eq update_r", "eq lead t2 + x/u"],
+       "1": ["loop update_r", "loop steps", "loop sum iq"],
+       "2": ["add: chain+coef", "add: J sweep", "add: R col+test"]}[det]
+for k, nm in [(5, lab[0]), (6, lab[1]), (7, lab[2]), (14, "eq add_constraint"),
               (15, "|h| chains (eq + loop)")]:
     print(f"    {nm:20s} mean {s[:, k].mean():10.0f}")
 it = db.iters.cpu().numpy()
