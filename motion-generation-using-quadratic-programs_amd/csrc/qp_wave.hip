@@ -495,9 +495,21 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   }
   // G -> R region (becomes L), g0 -> z region
   if (live && !pre) {
-    for (int e = ls; e < n * n; e += S) {
-      const int i = e / n, j = e - (e / n) * n;
-      L_(i, j) = EL(Gb, e);
+    if constexpr (NMAX <= S && NMAX <= 64) {
+      // lane j copies column j: every row's load issued at once (one memory latency; rows
+      // coalesced across lanes), indices clamped instead of predicated — the clamped loads and
+      // stores repeat row n-1 / column n-1 with the same values
+      const int jc = ls < n ? ls : n - 1;
+      double gv[NMAX];
+#pragma unroll
+      for (int i = 0; i < NMAX; i++) gv[i] = EL(Gb, (i < n ? i : n - 1) * n + jc);
+#pragma unroll
+      for (int i = 0; i < NMAX; i++) L_(i < n ? i : n - 1, jc) = gv[i];
+    } else {
+      for (int e = ls; e < n * n; e += S) {
+        const int i = e / n, j = e - (e / n) * n;
+        L_(i, j) = EL(Gb, e);
+      }
     }
     for (int i = ls; i < n; i += S) zv[i] = EL(g0b, i);
   }
