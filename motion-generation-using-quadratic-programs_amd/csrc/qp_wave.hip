@@ -860,8 +860,11 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           return kPackedR ? Rm + (i * n - (i * (i - 1)) / 2 - i) : Rm + i * JS;
         };
         double nd, nRii, nR1, nR[U], nr[U];  // the next row's values
+        // row i's base pointer (Ri[j] = R[i][j]), stepped per row: packed, row i-1 starts
+        // n - i entries before row i (no multiplications in the loop)
+        const double* Rp = rowp(iq - 1);
         auto prefetch = [&](int i) {
-          const double* Ri = rowp(i);
+          const double* Ri = Rp;
           nd = dv[i];
           nRii = Ri[i];
           nR1 = Ri[i + 1];
@@ -891,7 +894,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
             s += u < c ? q : 0.0;
           }
           if (c > U) {
-            const double* Ri = rowp(i);
+            const double* Ri = Rp;
             for (int jb = i + 2 + U; jb < iq; jb += U) {
               double aR[U], ar[U];
 #pragma unroll
@@ -908,6 +911,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
             }
           }
           const double r = (di - s) / Rii;
+          if (i > 0) Rp -= kPackedR ? n - i : JS;
           prefetch(i > 0 ? i - 1 : 0);  // r[i+1 ..] are in LDS already; r[i] is carried
           rv[i] = r;
           rn = r;
@@ -963,17 +967,18 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
     }
   };
   // the lead's two step dot products z.z and z.np, one pass (two independent chains)
-  auto dot2_lead = [&](double& zz, double& znp) {
-    double s1 = 0.0, s2 = 0.0;
+  auto dot2_lead = [&](double& zz, double& znp, double* npx = nullptr) {
+    double s1 = 0.0, s2 = 0.0, s3 = 0.0;
     constexpr int U = 8;  // loads of a chunk issued together (the adds stay in i order)
     // loads unconditional (in-bounds LDS past n), products past n replaced by +0.0: both sums
     // start at +0.0, so they are never -0.0 and adding +0.0 leaves them unchanged
     for (int ib = 0; ib < n; ib += U) {
-      double zc[U], pc[U];
+      double zc[U], pc[U], xc[U];
 #pragma unroll
       for (int u = 0; u < U; u++) {
         zc[u] = zv[ib + u];
         pc[u] = npv[ib + u];
+        if (npx) xc[u] = xv[ib + u];
       }
       const int c = n - ib;
 #pragma unroll
@@ -981,13 +986,15 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         const double q1 = zc[u] * zc[u], q2 = zc[u] * pc[u];
         s1 += u < c ? q1 : 0.0;
         s2 += u < c ? q2 : 0.0;
+        if (npx) {
+          const double q3 = pc[u] * xc[u];
+          s3 += u < c ? q3 : 0.0;
+        }
       }
     }
     zz = s1;
     znp = s2;
-  };
-  auto dot_lead = [&](const double* u_, const double* v_) {
-    return seq_fma_up_lds<8>(0.0, 0, n, [&](int i) { return u_[i]; }, [&](int i) { return v_[i]; });
+    if (npx) *npx = s3;
   };
   // add_constraint (@.text+0x21fd), split in three:
   //  1. the lead runs the serial part of the d-chain.  Rotation g (j = n-1-g) computes
@@ -1385,9 +1392,9 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       teq[1] += e2 - e1;
       if (lead) {
         const int iq = ctl->iq;
-        double t2 = 0.0, zz, znp;
-        dot2_lead(zz, znp);
-        if (fabs(zz) > kEps) t2 = (-dot_lead(npv, xv) - c0) / znp;
+        double t2 = 0.0, zz, znp, npx;
+        dot2_lead(zz, znp, &npx);  // np.x in the same pass (the reference's np.x, i ascending)
+        if (fabs(zz) > kEps) t2 = (-npx - c0) / znp;
         ctl->t2 = t2;
         uv[iq] = t2;
         ctl->f += 0.5 * (t2 * t2) * znp;
