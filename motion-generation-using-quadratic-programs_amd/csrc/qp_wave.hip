@@ -42,6 +42,10 @@ __device__ __forceinline__ void grp_sync() {
 #ifndef QPGPU_WAVE_KUJ
 #define QPGPU_WAVE_KUJ 4
 #endif
+// chunk of compute_d_z's LDS sums (J in LDS)
+#ifndef QPGPU_WAVE_KUDZ
+#define QPGPU_WAVE_KUDZ 8
+#endif
 constexpr int kUG = 8, kUL = QPGPU_WAVE_KUL;
 
 // s + sum_{j=j0}^{j1-1} A(j) * B(j), j ascending (s += a*b per element).  Full chunks of kU
@@ -830,11 +834,11 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
     } else {
       for (int c = ls; c < n; c += S)
         dv[c] = GJR ? seq_fma_up<KG>(0.0, 0, n, [&](int j) { return J_(j, c); }, [&](int j) { return npv[j]; })
-                    : seq_fma_up_lds<kUL>(0.0, 0, n, [&](int j) { return J_(j, c); }, [&](int j) { return npv[j]; });
+                    : seq_fma_up_lds<QPGPU_WAVE_KUDZ>(0.0, 0, n, [&](int j) { return J_(j, c); }, [&](int j) { return npv[j]; });
       grp_sync<S>();
       for (int r = ls; r < n; r += S)
         zv[r] = GJR ? seq_fma_up<KG>(0.0, iq, n, [&](int j) { return J_(r, j); }, [&](int j) { return dv[j]; })
-                    : seq_fma_up_lds<kUL>(0.0, iq, n, [&](int j) { return J_(r, j); }, [&](int j) { return dv[j]; });
+                    : seq_fma_up_lds<QPGPU_WAVE_KUDZ>(0.0, iq, n, [&](int j) { return J_(r, j); }, [&](int j) { return dv[j]; });
       grp_sync<S>();
     }
   };
@@ -970,9 +974,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   auto dot2_lead = [&](double& zz, double& znp, double* npx = nullptr) {
     double s1 = 0.0, s2 = 0.0, s3 = 0.0;
     constexpr int U = 8;  // loads of a chunk issued together (the adds stay in i order)
-    // loads unconditional (in-bounds LDS past n), products past n replaced by +0.0: both sums
-    // start at +0.0, so they are never -0.0 and adding +0.0 leaves them unchanged
-    for (int ib = 0; ib < n; ib += U) {
+    // full chunks, then the last one with unconditional loads (in-bounds LDS past n) and its
+    // products past n replaced by +0.0: the sums start at +0.0, so they are never -0.0 and
+    // adding +0.0 leaves them unchanged
+    auto chunk = [&](int ib, int c) {
       double zc[U], pc[U], xc[U];
 #pragma unroll
       for (int u = 0; u < U; u++) {
@@ -980,7 +985,6 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         pc[u] = npv[ib + u];
         if (npx) xc[u] = xv[ib + u];
       }
-      const int c = n - ib;
 #pragma unroll
       for (int u = 0; u < U; u++) {
         const double q1 = zc[u] * zc[u], q2 = zc[u] * pc[u];
@@ -991,7 +995,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           s3 += u < c ? q3 : 0.0;
         }
       }
-    }
+    };
+    int ib = 0;
+    for (; ib + U <= n; ib += U) chunk(ib, U);
+    if (ib < n) chunk(ib, n - ib);
     zz = s1;
     znp = s2;
     if (npx) *npx = s3;
@@ -1599,14 +1606,16 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       if (lead) {
         double psi = 0.0;
         constexpr int U = 8;  // loads of a chunk together, adds in i order
-        for (int ib = 0; ib < m; ib += U) {
+        auto chunk = [&](int ib, int c) {
           double sc[U];
 #pragma unroll
           for (int u = 0; u < U; u++) sc[u] = sv[ib + u];  // past m: in-bounds LDS, masked
-          const int c = m - ib;
 #pragma unroll
           for (int u = 0; u < U; u++) psi += (u < c && sc[u] < 0.0) ? sc[u] : 0.0;
-        }
+        };
+        int ib = 0;
+        for (; ib + U <= m; ib += U) chunk(ib, U);
+        if (ib < m) chunk(ib, m - ib);
         ctl->ss = 0.0;
         ctl->ip = 0;
         if (fabs(psi) <= (double)m * kEps * ctl->c1 * ctl->c2 * 100.0) {
