@@ -17,6 +17,8 @@
 #include <climits>
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "qp_common.h"
 
 namespace qpk {
@@ -879,8 +881,19 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           }
         };
         prefetch(iq - 1);
-        double rn = 0.0;  // r[i+1]
-        for (int i = iq - 1; i >= 0; i--) {
+        double rn;  // r[i+1]
+        {
+          // row iq-1: an empty sum (+0.0)
+          const double di = nd, Rii = nRii;
+          const double r = (di - 0.0) / Rii;
+          if (iq > 1) Rp -= kPackedR ? n - (iq - 1) : JS;
+          prefetch(iq > 1 ? iq - 2 : 0);
+          rv[iq - 1] = r;
+          rn = r;
+        }
+        // rows in two runs: chunk 0 partly past the row (c = iq-i-2 < U: masked), then whole
+        // (c >= U: unmasked, longer rows' further chunks with the last one masked)
+        auto row = [&](int i, auto Whole) {
           const double di = nd, Rii = nRii, R1 = nR1;
           double cR[U], cr[U];
 #pragma unroll
@@ -888,29 +901,33 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
             cR[u] = nR[u];
             cr[u] = nr[u];
           }
-          const double p1 = i + 1 < iq ? R1 * rn : 0.0;
           double s = 0.0;
-          s += p1;
-          const int c = iq - (i + 2);  // valid entries of the chunk
+          s += R1 * rn;
+          const int c = iq - (i + 2);  // valid entries of chunk 0
 #pragma unroll
           for (int u = 0; u < U; u++) {
             const double q = cR[u] * cr[u];
-            s += u < c ? q : 0.0;
+            if constexpr (decltype(Whole)::value)
+              s += q;
+            else
+              s += u < c ? q : 0.0;
           }
-          if (c > U) {
-            const double* Ri = Rp;
-            for (int jb = i + 2 + U; jb < iq; jb += U) {
-              double aR[U], ar[U];
+          if constexpr (decltype(Whole)::value) {
+            if (c > U) {
+              const double* Ri = Rp;
+              for (int jb = i + 2 + U; jb < iq; jb += U) {
+                double aR[U], ar[U];
 #pragma unroll
-              for (int u = 0; u < U; u++) {
-                aR[u] = Ri[jb + u];
-                ar[u] = rv[jb + u];
-              }
-              const int cc = iq - jb;
+                for (int u = 0; u < U; u++) {
+                  aR[u] = Ri[jb + u];
+                  ar[u] = rv[jb + u];
+                }
+                const int cc = iq - jb;
 #pragma unroll
-              for (int u = 0; u < U; u++) {
-                const double q = aR[u] * ar[u];
-                s += u < cc ? q : 0.0;
+                for (int u = 0; u < U; u++) {
+                  const double q = aR[u] * ar[u];
+                  s += u < cc ? q : 0.0;
+                }
               }
             }
           }
@@ -919,7 +936,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           prefetch(i > 0 ? i - 1 : 0);  // r[i+1 ..] are in LDS already; r[i] is carried
           rv[i] = r;
           rn = r;
-        }
+        };
+        int i = iq - 2;
+        for (; i >= 0 && iq - i - 2 < U; i--) row(i, std::false_type{});
+        for (; i >= 0; i--) row(i, std::true_type{});
       }
     } else if constexpr (!GJR) {
       if (lead)
