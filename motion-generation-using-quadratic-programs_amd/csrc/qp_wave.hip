@@ -314,7 +314,8 @@ struct WaveCfg {
 // class: 37 KiB per two-QP block instead of 42 KiB, i.e. 4 blocks per CU instead of 3, one
 // wave on every SIMD).  J and R are [n][js] with an odd row stride js, so walks down a column
 // (lane = row) are LDS-bank-conflict free; with GJR they live in the workspace instead.
-// Vectors: x z d np r x_old gc gs gx gf (n each), u u_old (n+1 each), s (m), then int A A_old
+// Vectors: x z d np r x_old (n each), the Givens coefficients (4n, interleaved per rotation),
+// u u_old (n+1 each), s (m), then int A A_old
 // (n+1 each), uint8 act exc (m each) and the control block.
 //
 // REGJ layout (J in registers, one row per lane; see kRegJ): R packed (upper triangle row by row,
@@ -446,10 +447,13 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   double* const npv = Q + Ly.off_np;
   double* const rv = Q + Ly.off_rv;
   double* const xo = Q + Ly.off_xo;
+  // Givens coefficients of rotation g interleaved (c, s, x, applied flag) at gc[4g..4g+3], so
+  // a rotation's four are one or two paired LDS accesses
   double* const gc = Q + Ly.off_gc;
-  double* const gs = gc + nv;
-  double* const gx = gs + nv;
-  double* const gf = gx + nv;  // Givens step applied (1.0) / skipped (0.0)
+#define GC_(g) gc[(g) * 4]
+#define GS_(g) gc[(g) * 4 + 1]
+#define GX_(g) gc[(g) * 4 + 2]
+#define GF_(g) gc[(g) * 4 + 3]  // Givens step applied (1.0) / skipped (0.0)
   double* const uv = Q + Ly.off_u;
   double* const uo = Q + Ly.off_uo;
   double* const sv = Q + Ly.off_s;
@@ -1056,8 +1060,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
             const double a0 = ac[u];
             const double h = qp_distance(a0, carried);
             const bool skip = fabs(h) < kEps;
-            gf[ng + u] = skip ? 0.0 : 1.0;
-            gx[ng + u] = h;
+            GF_(ng + u) = skip ? 0.0 : 1.0;
+            GX_(ng + u) = h;
             carried = skip ? a0 : h;
           }
           ng += U;
@@ -1066,8 +1070,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           const double a0 = dv[jb - 1];
           const double h = qp_distance(a0, carried);
           const bool skip = fabs(h) < kEps;
-          gf[ng] = skip ? 0.0 : 1.0;
-          gx[ng] = h;
+          GF_(ng) = skip ? 0.0 : 1.0;
+          GX_(ng) = h;
           carried = skip ? a0 : h;
           ng++;
         }
@@ -1084,8 +1088,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
               const double a0 = ac[u];
               const double h = qp_distance(a0, carried);
               const bool skip = fabs(h) < kEps;
-              gf[ng] = skip ? 0.0 : 1.0;
-              gx[ng] = h;
+              GF_(ng) = skip ? 0.0 : 1.0;
+              GX_(ng) = h;
               carried = skip ? a0 : h;
               ng++;
             }
@@ -1101,14 +1105,14 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       double cc = 0.0, ss = 0.0, xny = 0.0, dlast = 0.0;
       if (mine) {
         const int j = n - 1 - g;
-        const double h = gx[g], cc_raw = dv[j - 1];
+        const double h = GX_(g), cc_raw = dv[j - 1];
         double ss_raw = dv[j];
-        if (g > 0 && gf[g - 1] != 0.0) {
-          const double hp = gx[g - 1];
+        if (g > 0 && GF_(g - 1) != 0.0) {
+          const double hp = GX_(g - 1);
           ss_raw = (dv[j] / hp < 0.0) ? -hp : hp;
         }
         dlast = cc_raw;
-        if (gf[g] != 0.0) {
+        if (GF_(g) != 0.0) {
           ss = ss_raw / h;
           cc = cc_raw / h;
           if (cc < 0.0) {
@@ -1123,9 +1127,9 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       }
       grp_sync<S>();
       if (mine) {
-        gc[g] = cc;
-        gs[g] = ss;
-        gx[g] = xny;
+        GC_(g) = cc;
+        GS_(g) = ss;
+        GX_(g) = xny;
         if (g == ng - 1) dv[n - 1 - g - 1] = dlast;  // d[iq] after the sweep
       }
     }
@@ -1142,8 +1146,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           const int g = n - 1 - j;
           const bool on = j <= n - 1 && j >= iq0 + 1;
           const int gi = on ? g : 0;
-          const double c = gc[gi], sn = gs[gi], xn = gx[gi];
-          const bool f = on && gf[gi] != 0.0;
+          const double c = GC_(gi), sn = GS_(gi), xn = GX_(gi);
+          const bool f = on && GF_(gi) != 0.0;
           const double t1 = Jr[j - 1], t2 = Jr[j];
           const double n1 = t1 * c + t2 * sn;
           Jr[j - 1] = f ? n1 : t1;
@@ -1166,10 +1170,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
 #pragma unroll
           for (int u = 0; u < kU; u++) {
             t1v[u] = J_(k, n - 2 - g - u);
-            cv[u] = gc[g + u];
-            sw[u] = gs[g + u];
-            xw[u] = gx[g + u];
-            fw[u] = gf[g + u] != 0.0;
+            cv[u] = GC_(g + u);
+            sw[u] = GS_(g + u);
+            xw[u] = GX_(g + u);
+            fw[u] = GF_(g + u) != 0.0;
           }
 #pragma unroll
           for (int u = 0; u < kU; u++) {
@@ -1181,8 +1185,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         }
         for (; g < ng; g++) {
           const double t1 = J_(k, n - 2 - g), t2 = carry;
-          const double c = gc[g], sn = gs[g], xn = gx[g];
-          const bool f = gf[g] != 0.0;
+          const double c = GC_(g), sn = GS_(g), xn = GX_(g);
+          const bool f = GF_(g) != 0.0;
           const double n1 = t1 * c + t2 * sn;
           J_(k, n - 1 - g) = f ? xn * (t1 + n1) - t2 : t2;
           carry = f ? n1 : t1;
@@ -1210,10 +1214,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
             const bool ok = g < ng;
             t1v[u] = ok ? J_(k, n - 2 - g) : 0.0;
             if constexpr (!GJR) {
-              cv[u] = ok ? gc[g] : 0.0;
-              sw[u] = ok ? gs[g] : 0.0;
-              xw[u] = ok ? gx[g] : 0.0;
-              fw[u] = ok && gf[g] != 0.0;
+              cv[u] = ok ? GC_(g) : 0.0;
+              sw[u] = ok ? GS_(g) : 0.0;
+              xw[u] = ok ? GX_(g) : 0.0;
+              fw[u] = ok && GF_(g) != 0.0;
             }
           }
 #pragma unroll
@@ -1222,10 +1226,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
             if (g < ng) {
               const int uc = GJR ? 0 : u;
               if constexpr (GJR) {
-                cv[0] = gc[g];
-                sw[0] = gs[g];
-                xw[0] = gx[g];
-                fw[0] = gf[g] != 0.0;
+                cv[0] = GC_(g);
+                sw[0] = GS_(g);
+                xw[0] = GX_(g);
+                fw[0] = GF_(g) != 0.0;
               }
               const double t1 = t1v[u], t2 = carry;
               const double n1 = t1 * cv[uc] + t2 * sw[uc];
@@ -1302,7 +1306,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           double cc = R_(j, j), ss = R_(j + 1, j);
           const double h = qp_distance(cc, ss);
           if (fabs(h) < kEps) {
-            gf[ng++] = 0.0;
+            GF_(ng++) = 0.0;
             continue;
           }
           cc = cc / h;
@@ -1322,10 +1326,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
             R_(j, k) = r1;
             R_(j + 1, k) = xny * (t1 + r1) - t2;
           }
-          gc[ng] = cc;
-          gs[ng] = ss;
-          gx[ng] = xny;
-          gf[ng++] = 1.0;
+          GC_(ng) = cc;
+          GS_(ng) = ss;
+          GX_(ng) = xny;
+          GF_(ng++) = 1.0;
         }
       }
       ctl->ngiv = ng;
@@ -1344,8 +1348,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
             const int g = j - qq;
             const bool on = g >= 0 && g < ng;
             const int gi = on ? g : 0;
-            const double c = gc[gi], sn = gs[gi], xn = gx[gi];
-            const bool f = on && gf[gi] != 0.0;
+            const double c = GC_(gi), sn = GS_(gi), xn = GX_(gi);
+            const bool f = on && GF_(gi) != 0.0;
             const double t1 = Jr[j], t2 = Jr[j + 1];
             const double n1 = t1 * c + t2 * sn;
             Jr[j] = f ? n1 : t1;
@@ -1366,10 +1370,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
             const bool ok = g < ng;
             t2v[u] = ok ? J_(k, qq + g + 1) : 0.0;
             if constexpr (!GJR) {
-              cv[u] = ok ? gc[g] : 0.0;
-              sw[u] = ok ? gs[g] : 0.0;
-              xw[u] = ok ? gx[g] : 0.0;
-              fw[u] = ok && gf[g] != 0.0;
+              cv[u] = ok ? GC_(g) : 0.0;
+              sw[u] = ok ? GS_(g) : 0.0;
+              xw[u] = ok ? GX_(g) : 0.0;
+              fw[u] = ok && GF_(g) != 0.0;
             }
           }
 #pragma unroll
@@ -1378,10 +1382,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
             if (g < ng) {
               const int uc = GJR ? 0 : u;
               if constexpr (GJR) {
-                cv[0] = gc[g];
-                sw[0] = gs[g];
-                xw[0] = gx[g];
-                fw[0] = gf[g] != 0.0;
+                cv[0] = GC_(g);
+                sw[0] = GS_(g);
+                xw[0] = GX_(g);
+                fw[0] = GF_(g) != 0.0;
               }
               const double t1 = carry, t2 = t2v[u];
               const double n1 = t1 * cv[uc] + t2 * sw[uc];
@@ -1853,6 +1857,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   }
 #undef J_
 #undef R_
+#undef GC_
+#undef GS_
+#undef GX_
+#undef GF_
 
   qp_stamp(a, 4);
   if (a.stamps && threadIdx.x == 0)
