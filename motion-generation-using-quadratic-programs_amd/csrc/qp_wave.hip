@@ -270,6 +270,11 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
 #ifndef QPGPU_WAVE_URU
 #define QPGPU_WAVE_URU 4
 #endif
+// per-phase clocks of the diagnostic stamps (tools/stamps_wave.py; off in the product build:
+// their accumulators cost ~50 VGPRs, which the l1 scan's 16-row chunks use instead)
+#ifndef QPGPU_WAVE_STAMPS
+#define QPGPU_WAVE_STAMPS 0
+#endif
 // add_constraint's |h| chain in unmasked chunks + a one-rotation tail, qp_distance_f
 #ifndef QPGPU_WAVE_HCHAIN2
 #define QPGPU_WAVE_HCHAIN2 1
@@ -280,7 +285,10 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
 #endif
 // CI loads per chunk of the two-constraint l1 scan (one global-memory round trip per chunk)
 #ifndef QPGPU_WAVE_SCANKG
-#define QPGPU_WAVE_SCANKG 8
+#define QPGPU_WAVE_SCANKG 16
+#endif
+#ifndef QPGPU_WAVE_SCANKG4  // the 128-VGPR (four waves per SIMD) instantiations
+#define QPGPU_WAVE_SCANKG4 16
 #endif
 // diagnostic stamps only: slots 5..7 hold, instead of the equality-phase parts, the loop's
 // update_r cycles, step count and sum of iq over steps (1), or add_constraint's |h| chain +
@@ -792,7 +800,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   // diagnostic clocks (stamps only): loop phases (scan, select, d/z, lead step, add, delete) and
   // equality-phase parts (d/z, update_r, lead t2 + x/u, add_constraint, the lead's |h| chains)
   uint64_t tph[6] = {0, 0, 0, 0, 0, 0}, teq[5] = {0, 0, 0, 0, 0}, tdet[3] = {0, 0, 0};
-  auto clk = [&]() -> uint64_t { return a.stamps ? __builtin_amdgcn_s_memtime() : 0; };
+  auto clk = [&]() -> uint64_t { return (QPGPU_WAVE_STAMPS && a.stamps) ? __builtin_amdgcn_s_memtime() : 0; };
   auto compute_d_z = [&](int iq) {
     if constexpr (kRegJ) {
       // d[c] = sum_j J[j][c] np[j] (j ascending) with row j in lane j's registers: the products
@@ -1102,29 +1110,20 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
     {
       const int ng = ctl->ngiv, g = ls;
       const bool mine = g < ng;
-      double cc = 0.0, ss = 0.0, xny = 0.0, dlast = 0.0;
-      if (mine) {
-        const int j = n - 1 - g;
-        const double h = GX_(g), cc_raw = dv[j - 1];
-        double ss_raw = dv[j];
-        if (g > 0 && GF_(g - 1) != 0.0) {
-          const double hp = GX_(g - 1);
-          ss_raw = (dv[j] / hp < 0.0) ? -hp : hp;
-        }
-        dlast = cc_raw;
-        if (GF_(g) != 0.0) {
-          ss = ss_raw / h;
-          cc = cc_raw / h;
-          if (cc < 0.0) {
-            cc = -cc;
-            ss = -ss;
-            dlast = -h;
-          } else {
-            dlast = h;
-          }
-          xny = ss / (1.0 + cc);
-        }
-      }
+      // branch-free: every lane evaluates both branches of the reference's rotation with its
+      // index clamped (lanes past ng compute values nobody stores) and selects
+      const int gm = mine ? g : 0, gp = gm > 0 ? gm - 1 : 0;
+      const int j = n - 1 - gm;
+      const double h = GX_(gm), cc_raw = dv[j - 1], dj = dv[j], hp = GX_(gp);
+      const bool prev = gm > 0 && GF_(gp) != 0.0, app = GF_(gm) != 0.0;
+      const double ss_raw = prev ? ((dj / hp < 0.0) ? -hp : hp) : dj;
+      double ss1 = ss_raw / h, cc1 = cc_raw / h;
+      const bool neg = cc1 < 0.0;
+      cc1 = neg ? -cc1 : cc1;
+      ss1 = neg ? -ss1 : ss1;
+      const double x1 = ss1 / (1.0 + cc1);
+      const double cc = app ? cc1 : 0.0, ss = app ? ss1 : 0.0, xny = app ? x1 : 0.0;
+      const double dlast = app ? (neg ? -h : h) : cc_raw;
       grp_sync<S>();
       if (mine) {
         GC_(g) = cc;
@@ -1575,7 +1574,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         const bool h0 = i0 < m, h1 = i1 < m;
         const int c0i = h0 ? i0 : 0, c1i = h1 ? i1 : c0i;
         const double c00 = EL(ci0b, c0i), c01 = EL(ci0b, c1i);
-        constexpr int SKG = QPGPU_WAVE_SCANKG;
+        constexpr int SKG = OCC >= 4 ? QPGPU_WAVE_SCANKG4 : QPGPU_WAVE_SCANKG;
         double s0 = 0.0, s1 = 0.0;
         int jb = 0;
         for (; jb + SKG <= n; jb += SKG) {
@@ -1907,7 +1906,12 @@ static hipError_t launch_wave(const QpArgs& a, hipStream_t stream, double* ws) {
   // keeps the unconstrained allocation (21.0 vs 22.0 ms).  The register-setup instantiations
   // (OCC 2 for S = 16, OCC 1) use the packed-R layout when QPGPU_WAVE_RPACK is on.
   if constexpr (S < 64 && !GJR) {
-    if (lds_bytes <= 20480) {
+    // QPGPU_WAVE_OCC4_LDS (diagnostic) moves the 20 KiB threshold
+    static const size_t occ4_lds = [] {
+      const char* e = getenv("QPGPU_WAVE_OCC4_LDS");
+      return e ? (size_t)atol(e) : (size_t)20480;
+    }();
+    if (lds_bytes <= occ4_lds) {
       hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR, 4>), dim3((unsigned)blocks), dim3(C::BS),
                          lds_bytes, stream, a, ws);
       return hipGetLastError();

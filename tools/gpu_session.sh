@@ -82,7 +82,8 @@ for s in $STEPS; do
       run wave_parity 900 python -m pytest tests/test_gpu_parity.py -m gpu -q -x -rf -k "wave or config_parity or large_config or panel or edge or tail"
       run bench_C3 600 python bench.py --config C3 --no-cpu --steps 10 --warmup 3
       run bench_mgqp 600 python bench.py --config mgqp --no-cpu --steps 20
-      run stamps_C3 300 python tools/stamps_wave.py 30 6 60 65536 ;;
+      # stamps need the per-phase clocks compiled in: SRC=qp_wave tools/ab_build.sh stamps -DQPGPU_WAVE_STAMPS=1
+      if [ -f _ab/stamps/libqpgpu.so ]; then QPGPU_LIB_PATH=_ab/stamps/libqpgpu.so run stamps_C3 300 python tools/stamps_wave.py 30 6 60 65536; fi ;;
     abwstamps)
       run wstamps_base 300 python tools/stamps_wave.py ${WSHAPE:-30 6 60 65536}
       for v in ${VARIANTS}; do QPGPU_LIB_PATH=_ab/$v/libqpgpu.so run wstamps_$v 300 python tools/stamps_wave.py ${WSHAPE:-30 6 60 65536}; done ;;
