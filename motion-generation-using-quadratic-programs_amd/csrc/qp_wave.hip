@@ -270,6 +270,10 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
 #ifndef QPGPU_WAVE_URU
 #define QPGPU_WAVE_URU 4
 #endif
+// the select after a scan prepared inside the scan (argmin, np gather, ci0[ip] in flight early)
+#ifndef QPGPU_WAVE_PRESEL
+#define QPGPU_WAVE_PRESEL 1
+#endif
 // per-phase clocks of the diagnostic stamps (tools/stamps_wave.py; off in the product build:
 // their accumulators cost ~50 VGPRs, which the l1 scan's 16-row chunks use instead)
 #ifndef QPGPU_WAVE_STAMPS
@@ -1471,6 +1475,12 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   const int max_steps = a.max_steps;
   [[maybe_unused]] double cir[kCU][kCiReg ? NMAX : 1], c0r[kCU];
   [[maybe_unused]] bool ci_in_regs = false;
+  // the select that follows a scan (carried ss reset to 0): its argmin, the np gather and
+  // ci0[ip] are started inside the scan, so their global loads overlap the lead's psi sum
+  constexpr bool kPreSel = QPGPU_WAVE_PRESEL && kLaneSel && !GJR && MMAX <= 2 * S && NMAX <= S;
+  [[maybe_unused]] double pre_sb = 0.0, pre_np = 0.0, pre_c0 = 0.0;
+  [[maybe_unused]] int pre_ib = INT_MAX;
+  [[maybe_unused]] bool from_scan = false;
   // A QP falls through scan -> select -> step within one pass of the loop (QPGPU_WAVE_FALLTHRU),
   // so two QPs of a wave at different phases share the later blocks instead of running them in
   // separate passes.
@@ -1607,13 +1617,36 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
               s1 += a1[u] * xw[u];
             }
         }
+        const double v0 = s0 + c00, v1 = s1 + c01;
         if (h0) {
-          sv[i0] = s0 + c00;
+          sv[i0] = v0;
           exc[i0] = 0;
         }
         if (h1) {
-          sv[i1] = s1 + c01;
+          sv[i1] = v1;
           exc[i1] = 0;
+        }
+        if constexpr (kPreSel) {
+          // the select's candidates (s < 0, not active; exclusions were just cleared) from this
+          // lane's two sums in index order, then the subgroup argmin (ties: lower index)
+          sg_sync();  // the other lanes' act[] marks of this scan
+          double sb = inf;
+          int ib = INT_MAX;
+          if (h0 && v0 < 0.0 && !act[i0]) {
+            sb = v0;
+            ib = i0;
+          }
+          if (h1 && v1 < 0.0 && !act[i1] && v1 < sb) {
+            sb = v1;
+            ib = i1;
+          }
+          sg_argmin<S>(sb, ib);
+          pre_sb = sb;
+          pre_ib = ib;
+          const int ig = ib != INT_MAX ? ib : 0;
+          pre_np = EL(CIb, (ls < n ? ls : n - 1) * m + ig);
+          pre_c0 = EL(ci0b, ig);
+          from_scan = true;
         }
       } else {
         for (int i = ls; i < m; i += S) {
@@ -1659,17 +1692,22 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       [[maybe_unused]] double sbest = inf;
       [[maybe_unused]] int ibest = INT_MAX;
       if constexpr (kLaneSel) {
-        // each lane scans its constraints in index order, then the subgroup argmin: the same
-        // (smallest s below the carried ss, first index) as the reference's sequential scan
-        const double ss0 = ctl->ss;
-        for (int i = ls; i < m; i += S) {
-          const double v = sv[i];
-          if (v < ss0 && !act[i] && !exc[i] && v < sbest) {
-            sbest = v;
-            ibest = i;
+        if (kPreSel && from_scan) {
+          sbest = pre_sb;
+          ibest = pre_ib;
+        } else {
+          // each lane scans its constraints in index order, then the subgroup argmin: the same
+          // (smallest s below the carried ss, first index) as the reference's sequential scan
+          const double ss0 = ctl->ss;
+          for (int i = ls; i < m; i += S) {
+            const double v = sv[i];
+            if (v < ss0 && !act[i] && !exc[i] && v < sbest) {
+              sbest = v;
+              ibest = i;
+            }
           }
+          sg_argmin<S>(sbest, ibest);
         }
-        sg_argmin<S>(sbest, ibest);
       }
       if (lead) {
         double ss = ctl->ss;
@@ -1693,16 +1731,21 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         } else {
           uv[ctl->iq] = 0.0;
           Av[ctl->iq] = ip;
-          ctl->ci0ip = EL(ci0b, ip);
+          ctl->ci0ip = (kPreSel && from_scan) ? pre_c0 : EL(ci0b, ip);
           ctl->phase = PH_STEP;
         }
       }
       grp_sync<S>();
       if (ctl->phase == PH_STEP) {
         const int ip = ctl->ip;
-        for (int j = ls; j < n; j += S) npv[j] = EL(CIb, j * m + ip);
+        if (kPreSel && from_scan) {
+          if (ls < n) npv[ls] = pre_np;
+        } else {
+          for (int j = ls; j < n; j += S) npv[j] = EL(CIb, j * m + ip);
+        }
         grp_sync<S>();
       }
+      from_scan = false;
       tph[1] += clk() - t0;
       if (!QPGPU_WAVE_FALLTHRU) continue;
       phase = ctl->phase;

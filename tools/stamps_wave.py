@@ -1,7 +1,10 @@
 """Diagnostic: per-phase s_memtime stamps of the qp_wave kernel (qpgpu_debug_set_stamps).
 
 usage: python tools/stamps_wave.py N P M BATCH   (default C3: 30 6 60 65536)
-Prints cycles per block for: loads + Cholesky, J = L^-T + unconstrained solve, equality phase,
+Needs a library built with the per-phase clocks (SRC=qp_wave tools/ab_build.sh stamps
+-DQPGPU_WAVE_STAMPS=1, run with QPGPU_LIB_PATH=_ab/stamps/libqpgpu.so); the product build keeps
+only the phase-boundary stamps.  Prints cycles per block for: loads + Cholesky, J = L^-T +
+unconstrained solve, equality phase,
 active-set loop.  Never used for timing numbers."""
 import ctypes
 import os
