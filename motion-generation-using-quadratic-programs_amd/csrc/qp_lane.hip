@@ -107,6 +107,13 @@ constexpr int kScanDepth = QPGPU_SCAN_DEPTH;
 #ifndef QPGPU_LANE_HCHAIN
 #define QPGPU_LANE_HCHAIN 0
 #endif
+// p = 0: issue the CI / ci0 cache warm-up as soon as G has landed (before the Cholesky) and
+// retire its registers after the active-set loop, whose first scan waits for it anyway.
+// Measured on C2 (profiles/r02_s46): kernel 75.1 -> 82.0 us (3-stream steps 54.4 -> 52.9 us):
+// off
+#ifndef QPGPU_LANE_PF_P0
+#define QPGPU_LANE_PF_P0 0
+#endif
 // issue the CI / ci0 cache warm-up right after the G / CE staging instead of after the setup.
 // Measured slower (C1 kernel 54.0 -> 56.5 us, setup 21.7k -> 33.4k cycles/wave: vmcnt waits are
 // in issue order, so the G / CE waits then cover the warm-up loads too): off.
@@ -138,6 +145,8 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   constexpr bool kJregLoopCfg = QPGPU_LANE_JREG_LOOP == 2 || (QPGPU_LANE_JREG_LOOP == 1 && PX == 0);
   constexpr bool kRbRegs = QPGPU_LANE_RB_REGS == 2 || (QPGPU_LANE_RB_REGS == 1 && PX != 0);
   constexpr bool kLanePrefetch = QPGPU_LANE_PREFETCH == 1 || (QPGPU_LANE_PREFETCH == 2 && PX > 0);
+  // p = 0 (no equality phase): the warm-up right after G lands, retired after the loop
+  constexpr bool kPfP0 = QPGPU_LANE_PF_P0 && PX == 0 && !kLanePrefetch;
   static_assert(QPW == 64 || (QPW == 32 && T == 1), "half waves only with the QP-major layout");
   static_assert(MM <= 64, "bitmask bookkeeping holds m <= 64");
   using RI = RIdx<NM>;
@@ -233,7 +242,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
   // lanes of every wave at about the same time — reads L2 / MALL instead of queueing on one
   // chip-wide HBM burst.
   auto warmup = [&]() {
-  if constexpr (T == 1 && kLanePrefetch) {
+  if constexpr (T == 1 && (kLanePrefetch || kPfP0)) {
     if (live) {
       const char* c = reinterpret_cast<const char*>(a.CI + b * (int64_t)(n * m));
       const char* c0 = reinterpret_cast<const char*>(a.ci0 + b * (int64_t)m);
@@ -267,6 +276,7 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
       g0v[i] = (live && i < n) ? rd_all(offg0, n, i) : 0.0;
     }
     __syncthreads();
+    if constexpr (kPfP0) warmup();
     // round B: CE and ce0 (equality phase), issued now so they land during the Cholesky
     if (p > 0) {
       const int np_ = n * p;
@@ -1015,6 +1025,11 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
           }
         }
       }
+    }
+    if constexpr (T == 1 && kPfP0) {
+      if (live)  // the warm-up loads retire here (the first scan waited for them already)
+#pragma unroll
+        for (int k = 0; k < kPfCI + kPfC0; k++) asm volatile("" ::"v"(pf[k]));
     }
     if (a.stamps && lane == 0) {
       a.stamps[(uint64_t)blockIdx.x * kStampSlots + 5] = tscan;
