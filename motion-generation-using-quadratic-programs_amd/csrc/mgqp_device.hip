@@ -414,24 +414,31 @@ __global__ __launch_bounds__(64) void finish_level_reg_kernel(Plan P, Work W, co
   }
 }
 
-// Z = I - V V^T from the V workspace (rows of V: N, columns: R), for robots still active.
-template <int N>
-__global__ __launch_bounds__(64) void zform_kernel(Work W, int R) {
+// Z = I - V V^T from the V workspace (rows of V: N, columns: R), for robots still active.  V is
+// read once into registers (one robot per lane: 1 024 waves for 65 536 robots, one per SIMD, so
+// the N*R doubles cost no occupancy); Z is symmetric bit for bit (each entry sums the same
+// products V[i][l]*V[j][l] in l order), so the upper triangle is formed and stored twice.
+template <int N, int R>
+__global__ __launch_bounds__(64) void zform_kernel(Work W) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t K = W.count;
   if (r >= K || W.state[r] != 0) return;
-  for (int i = 0; i < N; ++i) {
-    double vi[N];
+  double v[N][R];
 #pragma unroll
-    for (int l = 0; l < N; ++l) vi[l] = l < R ? W.V[((int64_t)i * R + l) * K + r] : 0.0;
-    for (int j = 0; j < N; ++j) {
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int l = 0; l < R; ++l) v[i][l] = W.V[((int64_t)i * R + l) * K + r];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = i; j < N; ++j) {
       double sum = 0;
 #pragma unroll
-      for (int l = 0; l < N; ++l)
-        if (l < R) sum += vi[l] * W.V[((int64_t)j * R + l) * K + r];
-      W.Z[((int64_t)i * N + j) * K + r] = (i == j ? 1.f : 0.f) - (float)sum;
+      for (int l = 0; l < R; ++l) sum += v[i][l] * v[j][l];
+      const float z = (i == j ? 1.f : 0.f) - (float)sum;
+      W.Z[((int64_t)i * N + j) * K + r] = z;
+      if (j != i) W.Z[((int64_t)j * N + i) * K + r] = z;
     }
-  }
 }
 
 __global__ void outputs_kernel(Plan P, Work W, float* torques, float* tracking, int32_t* codes) {
@@ -481,7 +488,7 @@ bool try_finish_level_reg(const Plan& P, const Work& W, const double* x1, const 
   if (P.dim != N || acc_rows != R) return false;
   hipLaunchKernelGGL((finish_level_reg_kernel<N, R>), grid_for(W.count, 64), dim3(64), 0, s, P,
                      W, x1, f1, st1, x2, f2, st2, acc_rows);
-  hipLaunchKernelGGL(zform_kernel<N>, grid_for(W.count, 64), dim3(64), 0, s, W, R);
+  hipLaunchKernelGGL((zform_kernel<N, R>), grid_for(W.count, 64), dim3(64), 0, s, W);
   return true;
 }
 
