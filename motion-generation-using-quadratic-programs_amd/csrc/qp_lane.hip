@@ -107,6 +107,12 @@ constexpr int kScanDepth = QPGPU_SCAN_DEPTH;
 #ifndef QPGPU_LANE_HCHAIN
 #define QPGPU_LANE_HCHAIN 0
 #endif
+// add_constraint's Givens rotations branch-free (both outcomes selected) with the |h| chain
+// carried, so consecutive rotations could overlap.  Measured (profiles/r02_s50): C1 kernel
+// 51.7 vs 51.9 us, equality phase 24.8k -> 25.8k cycles per wave: off
+#ifndef QPGPU_LANE_ADDBF
+#define QPGPU_LANE_ADDBF 0
+#endif
 // p = 0: issue the CI / ci0 cache warm-up as soon as G has landed (before the Cholesky) and
 // retire its registers after the active-set loop, whose first scan waits for it anyway.
 // Measured on C2 (profiles/r02_s46): kernel 75.1 -> 82.0 us (3-stream steps 54.4 -> 52.9 us):
@@ -475,6 +481,36 @@ __global__ void __launch_bounds__(64, QPW == 64 ? 1 : 2) qp_lane_kernel(const Qp
     if (iq >= n) return false;  // reference UB (p > n); reported as dependent
     // |d[j]| as the rotation at j sees it: the previous rotation's h (applied) or the original
     double carried = 0.0;
+    if constexpr (QPGPU_LANE_ADDBF) {
+      // branch-free rotations: both outcomes of the |h| < eps test computed and selected, so
+      // the compiler can overlap rotation j-1's distance() chain (fed by the carried |h|, no
+      // division on it) with rotation j's divisions and J update.  Same operations per branch.
+#pragma unroll
+      for (int j = NM - 1; j >= LO + 1; j--) {
+        if (j <= n - 1 && j >= iq + 1) {
+          const double cc0 = dv[j - 1], ss0 = dv[j];
+          const double h = qp_distance(cc0, j < n - 1 ? carried : ss0);
+          const bool app = !(fabs(h) < kEps);
+          carried = app ? h : cc0;
+          double ss = ss0 / h, cc = cc0 / h;
+          const bool neg = cc < 0.0;
+          cc = neg ? -cc : cc;
+          ss = neg ? -ss : ss;
+          dv[j] = app ? 0.0 : ss0;
+          dv[j - 1] = app ? (neg ? -h : h) : cc0;
+          const double xny = ss / (1.0 + cc);
+#pragma unroll
+          for (int k = 0; k < NM; k++)
+            if (k < n) {
+              const double t1 = Jat(InReg, k, j - 1), t2 = Jat(InReg, k, j);
+              const double n1 = t1 * cc + t2 * ss;
+              const double n2 = xny * (t1 + n1) - t2;
+              Jat(InReg, k, j - 1) = app ? n1 : t1;
+              Jat(InReg, k, j) = app ? n2 : t2;
+            }
+        }
+      }
+    } else
 #pragma unroll
     for (int j = NM - 1; j >= LO + 1; j--) {
       if (j <= n - 1 && j >= iq + 1) {
