@@ -283,6 +283,9 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
 #ifndef QPGPU_WAVE_HCHAIN2
 #define QPGPU_WAVE_HCHAIN2 1
 #endif
+#ifndef QPGPU_WAVE_HCU  // rotations per unmasked chunk of the |h| chain
+#define QPGPU_WAVE_HCU 8
+#endif
 // add_constraint's J sweep (J in LDS) in unmasked chunks + a one-rotation tail
 #ifndef QPGPU_WAVE_SWEEP2
 #define QPGPU_WAVE_SWEEP2 1
@@ -1061,7 +1064,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         // values loaded together), then the tail one rotation per trip; distance() with the
         // range-reduced sqrt (qp_common.h)
         double carried = dv[n - 1];
-        constexpr int U = 4;
+        constexpr int U = QPGPU_WAVE_HCU;
         int jb = n - 1;
         for (; jb - U >= iq; jb -= U) {
           double ac[U];
