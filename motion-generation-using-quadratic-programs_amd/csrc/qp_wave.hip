@@ -225,6 +225,40 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
   }
 }
 
+// Tolerance-mode loop kernels for the workspace variant (n > 64 after the MFMA panel setup, which
+// already gives up the reference's bits for north_star's 1e-10): update_r as a wave-wide tree
+// sum per row (no serial chain, no LDS round trip) and compute_d + update_z fused into one pass
+// over J (lane = row, column chunks tree-reduced), so J is read once per step instead of
+// 1 + (n - iq) / n times.  QPGPU_FLAG_EXACT keeps the serial, bit-exact sums.
+#ifndef QPGPU_WAVE_TOLLOOP
+#define QPGPU_WAVE_TOLLOOP 3  // bit 0: fused compute_d + update_z, bit 1: tree update_r
+#endif
+// v from the lane the DPP control CTRL selects (a full-row permutation: every lane valid)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+// Sum of v over the 64 lanes of this wave (all lanes active), the same value in every lane:
+// symmetric butterflies inside each 16-lane row (quad xor 1, xor 2, half-row mirror, row
+// mirror: every pair adds the same two operands), then the four row sums in row order
+__device__ __forceinline__ double wave_sum_f64(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  v += dpp_f64<0x140>(v);  // row_mirror
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+  double r[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    r[k] = __builtin_bit_cast(double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, 16 * k) << 32) |
+                                          (uint32_t)__builtin_amdgcn_readlane(lo, 16 * k));  // no sign extension
+  return ((r[0] + r[1]) + r[2]) + r[3];
+}
+
 // Register-resident setup for the one-wave variants (S <= 64, LDS J/R, launched at one wave per
 // SIMD so registers are plentiful): lane j keeps row j of G/L (Cholesky), lane r builds row r of
 // J = L^{-T} by column-oriented forward substitution, and cholesky_solve runs across the lanes
@@ -853,6 +887,43 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       }
       grp_sync<S>();
     } else {
+      if constexpr (GJR && (QPGPU_WAVE_TOLLOOP & 1) && S == 4 * 64 && NMAX <= S) {
+        if (pre && n >= 2 * 16) {  // the double-buffered partials fit the 4n Givens doubles
+          // tolerance mode: lane r holds row r of each chunk of kDC columns (column-major J:
+          // coalesced), d[c] = sum_r J[r][c] np[r] as per-wave tree sums + the four wave partials
+          // in wave order (LDS, double-buffered in the Givens scratch, which is free during a
+          // step), then z[r] += J[r][c] d[c] for c >= iq from the same registers, c ascending
+          // (the reference's order for z given d).  One pass over J.
+          constexpr int kDC = 16;
+          const int wv = ls >> 6;
+          const bool row = ls < n;
+          const double npr = row ? npv[ls] : 0.0;
+          double z = 0.0;
+          int buf = 0;
+          for (int c0 = 0; c0 < n; c0 += kDC, buf ^= 1) {
+            double jv[kDC];
+#pragma unroll
+            for (int u = 0; u < kDC; u++) jv[u] = (row && c0 + u < n) ? J_(ls, c0 + u) : 0.0;
+            double* const P = gc + buf * (4 * kDC);
+#pragma unroll
+            for (int u = 0; u < kDC; u++) {
+              const double w = wave_sum_f64(jv[u] * npr);
+              if ((ls & 63) == 0) P[wv * kDC + u] = w;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < kDC; u++) {
+              const int c = c0 + u;
+              const double d = ((P[u] + P[kDC + u]) + P[2 * kDC + u]) + P[3 * kDC + u];
+              if (ls == 0 && c < n) dv[c] = d;
+              z += (c >= iq && c < n) ? jv[u] * d : 0.0;
+            }
+          }
+          if (row) zv[ls] = z;
+          grp_sync<S>();
+          return;
+        }
+      }
       for (int c = ls; c < n; c += S)
         dv[c] = GJR ? seq_fma_up<KG>(0.0, 0, n, [&](int j) { return J_(j, c); }, [&](int j) { return npv[j]; })
                     : seq_fma_up_lds<QPGPU_WAVE_KUDZ>(0.0, 0, n, [&](int j) { return J_(j, c); }, [&](int j) { return npv[j]; });
@@ -972,6 +1043,54 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
     } else {
       if (ls >= 64) return;  // waves 1.. idle (they wait at the caller's grp_sync)
       constexpr int PU = (NMAX + 63) / 64;
+      if constexpr (QPGPU_WAVE_TOLLOOP & 2) {
+        if (pre) {
+          // tolerance mode: lane l holds r[j] for j = l + 64u in registers; row i's products
+          // R[i][j] r[j] (j in (i, iq)) are summed by the wave's tree (wave_sum_f64), so each row
+          // costs a tree sum and a division.  Rows are fetched kRD ahead (a register ring with
+          // compile-time slots) so the global loads' latency is off the chain.
+          constexpr int kRD = 4;
+          double rr[PU], ring[kRD][PU], rd[kRD], rg[kRD];
+#pragma unroll
+          for (int u = 0; u < PU; u++) rr[u] = 0.0;
+          auto fetch_row = [&](int i, double* dst, double& di, double& gi) {
+#pragma unroll
+            for (int u = 0; u < PU; u++) {
+              const int j = ls + 64 * u;
+              dst[u] = (i >= 0 && j > i && j < iq) ? R_(i, j) : 0.0;
+            }
+            di = i >= 0 ? dv[i] : 0.0;
+            gi = i >= 0 ? R_(i, i) : 1.0;
+          };
+#pragma unroll
+          for (int k = 0; k < kRD; k++) fetch_row(iq - 1 - k, ring[k], rd[k], rg[k]);
+          for (int i0 = iq - 1; i0 >= 0; i0 -= kRD) {
+#pragma unroll
+            for (int k = 0; k < kRD; k++) {
+              const int i = i0 - k;
+              if (i < 0) break;
+              double rc[PU];
+#pragma unroll
+              for (int u = 0; u < PU; u++) rc[u] = ring[k][u];
+              const double di = rd[k], gi = rg[k];
+              fetch_row(i - kRD, ring[k], rd[k], rg[k]);
+              double sl = 0.0;
+#pragma unroll
+              for (int u = 0; u < PU; u++) {
+                const int j = ls + 64 * u;
+                sl += (j > i && j < iq) ? rc[u] * rr[u] : 0.0;
+              }
+              const double ri = (di - wave_sum_f64(sl)) / gi;
+#pragma unroll
+              for (int u = 0; u < PU; u++)
+                if (ls + 64 * u == i) rr[u] = ri;
+              if (lead) rv[i] = ri;
+            }
+          }
+          sg_sync();
+          return;
+        }
+      }
       double* const P = gc;  // scratch (the Givens buffers are free during a step)
       double rn[PU], rc[PU];
       auto fetch = [&](int i) {
