@@ -230,6 +230,11 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
 // sum per row (no serial chain, no LDS round trip) and compute_d + update_z fused into one pass
 // over J (lane = row, column chunks tree-reduced), so J is read once per step instead of
 // 1 + (n - iq) / n times.  QPGPU_FLAG_EXACT keeps the serial, bit-exact sums.
+// workspace variant's J sweep: rotation coefficients loaded per chunk of this many rotations
+// with the chunk's J entries (0: per rotation, chunks of 16 J loads)
+#ifndef QPGPU_WAVE_GJR_COEF
+#define QPGPU_WAVE_GJR_COEF 0
+#endif
 #ifndef QPGPU_WAVE_TOLLOOP
 #define QPGPU_WAVE_TOLLOOP 3  // bit 0: fused compute_d + update_z, bit 1: tree update_r
 #endif
@@ -1322,7 +1327,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       // Row k's sweep over columns n-1 .. iq: rotation g maps (J[k][j-1], J[k][j]), j = n-1-g,
       // to (n1, xny (t1 + n1) - t2) and n1 is the next rotation's t2, so it is carried in a
       // register and the t1 loads (independent of the chain) are issued kU at a time.
-      constexpr int kU = GJR ? KG : QPGPU_WAVE_KUJ;
+      constexpr bool kGC = GJR && QPGPU_WAVE_GJR_COEF;  // workspace variant, coefficients per chunk
+      constexpr int kU = GJR ? (kGC ? QPGPU_WAVE_GJR_COEF : KG) : QPGPU_WAVE_KUJ;
       const int ng = ctl->ngiv;
       for (int k = ls; k < n; k += S) {
         double carry = J_(k, n - 1);
@@ -1330,7 +1336,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           // the chunk's J entries (and, with J in LDS, its rotation coefficients) are loaded
           // before its first store (LDS stores would otherwise fence every later load); the
           // workspace variant reads the coefficients per rotation (registers: its occupancy)
-          constexpr int kUC = GJR ? 1 : kU;
+          constexpr int kUC = (GJR && !kGC) ? 1 : kU;
           double t1v[kU], cv[kUC], sw[kUC], xw[kUC];
           bool fw[kUC];
 #pragma unroll
@@ -1338,7 +1344,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
             const int g = gb + u;
             const bool ok = g < ng;
             t1v[u] = ok ? J_(k, n - 2 - g) : 0.0;
-            if constexpr (!GJR) {
+            if constexpr (!GJR || kGC) {
               cv[u] = ok ? GC_(g) : 0.0;
               sw[u] = ok ? GS_(g) : 0.0;
               xw[u] = ok ? GX_(g) : 0.0;
@@ -1349,8 +1355,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           for (int u = 0; u < kU; u++) {
             const int g = gb + u;
             if (g < ng) {
-              const int uc = GJR ? 0 : u;
-              if constexpr (GJR) {
+              const int uc = (GJR && !kGC) ? 0 : u;
+              if constexpr (GJR && !kGC) {
                 cv[0] = GC_(g);
                 sw[0] = GS_(g);
                 xw[0] = GX_(g);
