@@ -50,6 +50,7 @@ for s in $STEPS; do
     trace3) run trace3 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace3" -o c1 -- python3 bench.py --steps 20 --warmup 5 --no-cpu ;;
     profC3) run profC3 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profC3" -o c3 -- python3 bench.py --config C3 --steps 5 --warmup 1 --no-cpu --streams 1 --kernel-reps 3 ;;
     profC5) run profC5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profC5" -o c5 -- python3 bench.py --config C5 --steps 3 --warmup 1 --no-cpu --streams 1 --kernel-reps 2 ;;
+    profC5) run profC5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profC5" -o c5 -- python3 bench.py --config C5 --steps 2 --warmup 1 --no-cpu --streams 1 --kernel-reps 2 ;;
     pmcC5)
       run pmcC5_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcC5_fetch" -o c5 -- python3 bench.py --config C5 --steps 2 --warmup 1 --no-cpu --streams 1 --kernel-reps 1
       run pmcC5_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcC5_write" -o c5 -- python3 bench.py --config C5 --steps 2 --warmup 1 --no-cpu --streams 1 --kernel-reps 1
