@@ -236,7 +236,8 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
 #define QPGPU_WAVE_GJR_COEF 0
 #endif
 #ifndef QPGPU_WAVE_TOLLOOP
-#define QPGPU_WAVE_TOLLOOP 3  // bit 0: fused compute_d + update_z, bit 1: tree update_r
+#define QPGPU_WAVE_TOLLOOP 7  // bit 0: fused compute_d + update_z, bit 1: tree update_r,
+                              // bit 2: add_constraint J sweep deferred into the next d/z pass
 #endif
 // v from the lane the DPP control CTRL selects (a full-row permutation: every lane valid)
 template <int CTRL>
@@ -377,10 +378,11 @@ struct WaveCfg {
 // algorithm only ever shifts as zeros), the compute_d transpose scratch [n][kCHS], the loop's
 // vectors, and x z d last — during the setup the factor L ([n][js], rows stride js) overlays
 // everything before x, which is dead until the loop.
+constexpr int kTolCh = 16;  // columns per tree-summed chunk of the tolerance-mode d/z pass
 constexpr int kCH = 8, kCHS = kCH + 1;  // compute_d columns per transpose chunk, scratch row stride
 struct WaveLay {
   int js, nr, off_r, off_sc, off_x, off_z, off_d, off_np, off_rv, off_xo, off_gc, off_u, off_uo, off_s,
-      off_a, off_fl, off_ctl, stride;
+      off_a, off_fl, off_ctl, off_tsc, stride;
 };
 __host__ __device__ inline WaveLay wave_lay(int n, int m, bool gjr, bool regj = false, bool rpack = false) {
   WaveLay L;
@@ -439,7 +441,9 @@ __host__ __device__ inline WaveLay wave_lay(int n, int m, bool gjr, bool regj = 
     L.off_d = L.off_z + n;
     L.off_ctl = L.off_d + n;
   }
-  L.stride = (L.off_ctl + (int)((sizeof(Ctl) + 7) / 8)) | 1;
+  // the workspace variant's tolerance-mode partial sums (two buffers of 4 waves x kTolCh)
+  L.off_tsc = L.off_ctl + (int)((sizeof(Ctl) + 7) / 8);
+  L.stride = (L.off_tsc + (gjr ? 2 * 4 * kTolCh : 0)) | 1;
   return L;
 }
 // packed-R index (REGJ): R[i][j] for j >= i, the subdiagonal R[j+1][j], else the write-only slot
@@ -847,6 +851,10 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   // equality-phase parts (d/z, update_r, lead t2 + x/u, add_constraint, the lead's |h| chains)
   uint64_t tph[6] = {0, 0, 0, 0, 0, 0}, teq[5] = {0, 0, 0, 0, 0}, tdet[3] = {0, 0, 0};
   auto clk = [&]() -> uint64_t { return (QPGPU_WAVE_STAMPS && a.stamps) ? __builtin_amdgcn_s_memtime() : 0; };
+  // iq0 of an add_constraint whose J sweep was deferred into the next d/z pass, or -1
+  // (tolerance mode, QPGPU_WAVE_TOLLOOP bit 2; the same value in every lane)
+  int pend = -1;
+  constexpr bool kDefer = GJR && (QPGPU_WAVE_TOLLOOP & 4) && (QPGPU_WAVE_TOLLOOP & 1) && S == 4 * 64 && NMAX <= S;
   auto compute_d_z = [&](int iq) {
     if constexpr (kRegJ) {
       // d[c] = sum_j J[j][c] np[j] (j ascending) with row j in lane j's registers: the products
@@ -893,36 +901,76 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       grp_sync<S>();
     } else {
       if constexpr (GJR && (QPGPU_WAVE_TOLLOOP & 1) && S == 4 * 64 && NMAX <= S) {
-        if (pre && n >= 2 * 16) {  // the double-buffered partials fit the 4n Givens doubles
+        if (pre && n >= 2 * 16) {
           // tolerance mode: lane r holds row r of each chunk of kDC columns (column-major J:
           // coalesced), d[c] = sum_r J[r][c] np[r] as per-wave tree sums + the four wave partials
-          // in wave order (LDS, double-buffered in the Givens scratch, which is free during a
-          // step), then z[r] += J[r][c] d[c] for c >= iq from the same registers, c ascending
-          // (the reference's order for z given d).  One pass over J.
-          constexpr int kDC = 16;
+          // in wave order (LDS, double-buffered), then z[r] += J[r][c] d[c] for c >= iq from the
+          // same registers.  One pass over J.  With a deferred add_constraint sweep (pend = its
+          // iq0, QPGPU_WAVE_TOLLOOP bit 2) the pass applies the sweep too: columns below iq0 are
+          // read as they are, then each chunk of rotations produces its final columns n-1-g in
+          // registers (stored back to J) and their d and z terms, and column iq0 gets the carry.
+          constexpr int kDC = kTolCh;
           const int wv = ls >> 6;
           const bool row = ls < n;
           const double npr = row ? npv[ls] : 0.0;
+          double* const T = Q + Ly.off_tsc;
           double z = 0.0;
           int buf = 0;
-          for (int c0 = 0; c0 < n; c0 += kDC, buf ^= 1) {
-            double jv[kDC];
-#pragma unroll
-            for (int u = 0; u < kDC; u++) jv[u] = (row && c0 + u < n) ? J_(ls, c0 + u) : 0.0;
-            double* const P = gc + buf * (4 * kDC);
+          // d (and z) for the kDC values v of this lane's row; col(u) = their column or -1
+          auto chunk = [&](const double* v, auto col) {
+            double* const P = T + buf * (4 * kDC);
+            buf ^= 1;
 #pragma unroll
             for (int u = 0; u < kDC; u++) {
-              const double w = wave_sum_f64(jv[u] * npr);
+              const double w = wave_sum_f64(v[u] * npr);
               if ((ls & 63) == 0) P[wv * kDC + u] = w;
             }
             __syncthreads();
 #pragma unroll
             for (int u = 0; u < kDC; u++) {
-              const int c = c0 + u;
+              const int c = col(u);
               const double d = ((P[u] + P[kDC + u]) + P[2 * kDC + u]) + P[3 * kDC + u];
-              if (ls == 0 && c < n) dv[c] = d;
-              z += (c >= iq && c < n) ? jv[u] * d : 0.0;
+              if (ls == 0 && c >= 0) dv[c] = d;
+              z += (c >= iq) ? v[u] * d : 0.0;
             }
+          };
+          const int ps = pend;
+          const int cA = ps >= 0 ? ps : n;
+          for (int c0 = 0; c0 < cA; c0 += kDC) {
+            double jv[kDC];
+#pragma unroll
+            for (int u = 0; u < kDC; u++) jv[u] = (row && c0 + u < cA) ? J_(ls, c0 + u) : 0.0;
+            chunk(jv, [&](int u) { return c0 + u < cA ? c0 + u : -1; });
+          }
+          if (ps >= 0) {
+            const int ng = ctl->ngiv;  // = n - 1 - ps
+            double carry = row ? J_(ls, n - 1) : 0.0;
+            for (int gb = 0; gb < ng; gb += kDC) {
+              double t1v[kDC], fv[kDC];
+#pragma unroll
+              for (int u = 0; u < kDC; u++) t1v[u] = (row && gb + u < ng) ? J_(ls, n - 2 - gb - u) : 0.0;
+#pragma unroll
+              for (int u = 0; u < kDC; u++) {
+                const int g = gb + u;
+                fv[u] = 0.0;
+                if (g < ng) {
+                  const double c = GC_(g), sn = GS_(g), xn = GX_(g);
+                  const bool f = GF_(g) != 0.0;
+                  const double t1 = t1v[u], t2 = carry;
+                  const double n1 = t1 * c + t2 * sn;
+                  fv[u] = f ? xn * (t1 + n1) - t2 : t2;
+                  carry = f ? n1 : t1;
+                  if (row) J_(ls, n - 1 - g) = fv[u];
+                }
+              }
+              chunk(fv, [&](int u) { return gb + u < ng ? n - 1 - gb - u : -1; });
+            }
+            if (row) J_(ls, ps) = carry;
+            double cv[kDC];
+#pragma unroll
+            for (int u = 0; u < kDC; u++) cv[u] = u == 0 ? carry : 0.0;
+            chunk(cv, [&](int u) { return u == 0 ? ps : -1; });
+            pend = -1;
           }
           if (row) zv[ls] = z;
           grp_sync<S>();
@@ -1267,6 +1315,59 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
     const uint64_t h1 = clk();
     if (QPGPU_WAVE_STAMPS_DETAIL == 2) tdet[0] += h1 - h0;
     const int iq0 = ctl->iq;
+    // tolerance mode: the J sweep waits for the next d/z pass (which reads J anyway) unless the
+    // constraint turns out degenerate (then delete_constraint needs the swept J right away)
+    const bool defer = kDefer && pre && n >= 2 * kTolCh;
+    auto plain_sweep = [&]() {
+      // Row k's sweep over columns n-1 .. iq: rotation g maps (J[k][j-1], J[k][j]), j = n-1-g,
+      // to (n1, xny (t1 + n1) - t2) and n1 is the next rotation's t2, so it is carried in a
+      // register and the t1 loads (independent of the chain) are issued kU at a time.
+      constexpr bool kGC = GJR && QPGPU_WAVE_GJR_COEF;  // workspace variant, coefficients per chunk
+      constexpr int kU = GJR ? (kGC ? QPGPU_WAVE_GJR_COEF : KG) : QPGPU_WAVE_KUJ;
+      const int ng = ctl->ngiv;
+      for (int k = ls; k < n; k += S) {
+        double carry = J_(k, n - 1);
+        for (int gb = 0; gb < ng; gb += kU) {
+          // the chunk's J entries (and, with J in LDS, its rotation coefficients) are loaded
+          // before its first store (LDS stores would otherwise fence every later load); the
+          // workspace variant reads the coefficients per rotation (registers: its occupancy)
+          constexpr int kUC = (GJR && !kGC) ? 1 : kU;
+          double t1v[kU], cv[kUC], sw[kUC], xw[kUC];
+          bool fw[kUC];
+#pragma unroll
+          for (int u = 0; u < kU; u++) {
+            const int g = gb + u;
+            const bool ok = g < ng;
+            t1v[u] = ok ? J_(k, n - 2 - g) : 0.0;
+            if constexpr (!GJR || kGC) {
+              cv[u] = ok ? GC_(g) : 0.0;
+              sw[u] = ok ? GS_(g) : 0.0;
+              xw[u] = ok ? GX_(g) : 0.0;
+              fw[u] = ok && GF_(g) != 0.0;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < kU; u++) {
+            const int g = gb + u;
+            if (g < ng) {
+              const int uc = (GJR && !kGC) ? 0 : u;
+              if constexpr (GJR && !kGC) {
+                cv[0] = GC_(g);
+                sw[0] = GS_(g);
+                xw[0] = GX_(g);
+                fw[0] = GF_(g) != 0.0;
+              }
+              const double t1 = t1v[u], t2 = carry;
+              const double n1 = t1 * cv[uc] + t2 * sw[uc];
+              // skipped step (gf = 0): both columns unchanged
+              J_(k, n - 1 - g) = fw[uc] ? xw[uc] * (t1 + n1) - t2 : t2;
+              carry = fw[uc] ? n1 : t1;
+            }
+          }
+        }
+        J_(k, n - 1 - ng) = carry;
+      }
+    };
     if (kRegJ && iq0 < n) {
       // the same sweep on lane k's register row: rotation g = n-1-j on columns (j-1, j), j from
       // n-1 down to iq+1, with the reference's operations; out-of-range steps leave both columns
@@ -1323,55 +1424,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         }
         J_(k, n - 1 - ng) = carry;
       }
-    } else if (iq0 < n) {
-      // Row k's sweep over columns n-1 .. iq: rotation g maps (J[k][j-1], J[k][j]), j = n-1-g,
-      // to (n1, xny (t1 + n1) - t2) and n1 is the next rotation's t2, so it is carried in a
-      // register and the t1 loads (independent of the chain) are issued kU at a time.
-      constexpr bool kGC = GJR && QPGPU_WAVE_GJR_COEF;  // workspace variant, coefficients per chunk
-      constexpr int kU = GJR ? (kGC ? QPGPU_WAVE_GJR_COEF : KG) : QPGPU_WAVE_KUJ;
-      const int ng = ctl->ngiv;
-      for (int k = ls; k < n; k += S) {
-        double carry = J_(k, n - 1);
-        for (int gb = 0; gb < ng; gb += kU) {
-          // the chunk's J entries (and, with J in LDS, its rotation coefficients) are loaded
-          // before its first store (LDS stores would otherwise fence every later load); the
-          // workspace variant reads the coefficients per rotation (registers: its occupancy)
-          constexpr int kUC = (GJR && !kGC) ? 1 : kU;
-          double t1v[kU], cv[kUC], sw[kUC], xw[kUC];
-          bool fw[kUC];
-#pragma unroll
-          for (int u = 0; u < kU; u++) {
-            const int g = gb + u;
-            const bool ok = g < ng;
-            t1v[u] = ok ? J_(k, n - 2 - g) : 0.0;
-            if constexpr (!GJR || kGC) {
-              cv[u] = ok ? GC_(g) : 0.0;
-              sw[u] = ok ? GS_(g) : 0.0;
-              xw[u] = ok ? GX_(g) : 0.0;
-              fw[u] = ok && GF_(g) != 0.0;
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < kU; u++) {
-            const int g = gb + u;
-            if (g < ng) {
-              const int uc = (GJR && !kGC) ? 0 : u;
-              if constexpr (GJR && !kGC) {
-                cv[0] = GC_(g);
-                sw[0] = GS_(g);
-                xw[0] = GX_(g);
-                fw[0] = GF_(g) != 0.0;
-              }
-              const double t1 = t1v[u], t2 = carry;
-              const double n1 = t1 * cv[uc] + t2 * sw[uc];
-              // skipped step (gf = 0): both columns unchanged
-              J_(k, n - 1 - g) = fw[uc] ? xw[uc] * (t1 + n1) - t2 : t2;
-              carry = fw[uc] ? n1 : t1;
-            }
-          }
-        }
-        J_(k, n - 1 - ng) = carry;
-      }
+    } else if (iq0 < n && !defer) {
+      plain_sweep();
     }
     grp_sync<S>();
     const uint64_t h2 = clk();
@@ -1395,6 +1449,14 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       }
     }
     grp_sync<S>();
+    if (defer && iq0 < n) {
+      if (ctl->fin) {
+        pend = iq0;
+      } else {
+        plain_sweep();
+        grp_sync<S>();
+      }
+    }
     if (QPGPU_WAVE_STAMPS_DETAIL == 2) tdet[2] += clk() - h2;
   };
   // delete_constraint (@.text+0x26a8) of constraint l: the lead does the bookkeeping and the
