@@ -39,10 +39,20 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--streams", type=int, default=3,
                     help="independent cycles pipelined over this many HIP streams (1 = serialized)")
+    ap.add_argument("--wide", action="store_true",
+                    help="angle limits +-20 rad and gains (10, 2), as tests/test_gpu_mgqp.py's wide case: "
+                         "level-0 QPs are then feasible for part of the robots, so their solves run the "
+                         "active-set loop instead of the retry snapshot")
     args = ap.parse_args()
 
+    def configure(ctl):
+        if args.wide:
+            ctl.setAngularLimits([20.0] * 7, [-20.0] * 7)
+            ctl.setGains(10, 2)
+        return ctl
+
     sc = mgqp.make_scenario(args.robots, seed=2026)
-    c = mgqp.ops_controller()
+    c = configure(mgqp.ops_controller())
     dsc = mgqp.DeviceScenario(sc, "cuda")
     S = max(1, args.streams)
     streams = [torch.cuda.Stream() for _ in range(S)]
@@ -73,11 +83,12 @@ def main():
            "value": args.robots / (ms * 1e-3), "unit": "cycles/s", "robots": args.robots,
            "ms_per_step": ms, "ms_per_cycle_serialized": ms_serial, "streams": S,
            "streams_outputs_identical": bool(same), "steps": args.steps, "warmup": args.warmup,
-           "written_frac": ok, "dtype": "f32 glue + f64 QPs", "data": "synthetic"}
+           "written_frac": ok, "dtype": "f32 glue + f64 QPs", "data": "synthetic",
+           "limits": "wide (+-20 rad, gains 10/2)" if args.wide else "ops/mgqp.ops"}
 
     if not args.no_host:
         hs = mgqp.make_scenario(args.host_robots, seed=2026)
-        ch = mgqp.ops_controller()
+        ch = configure(mgqp.ops_controller())
         ch.update_batched(hs)
         t = time.perf_counter()
         ch.update_batched(hs)
@@ -89,7 +100,7 @@ def main():
         import test_mgqp_host as th
 
         H = mgqp.load_library(th.build_harness())
-        cc = mgqp.ops_controller(library=H)
+        cc = configure(mgqp.ops_controller(library=H))
         chunk = 512
         cs = mgqp.make_scenario(chunk, seed=2026)
         done, t0 = 0, time.perf_counter()
