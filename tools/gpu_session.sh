@@ -36,6 +36,7 @@ for s in $STEPS; do
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c1 -- python3 bench.py --steps 20 --warmup 5 --no-cpu --streams 1 ;;
     profmgqp) run profmgqp 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profmgqp" -o mgqp -- python3 tools/bench_mgqp.py --steps 3 --no-host --no-cpu ;;
     benchmgqp) run benchmgqp 600 python tools/bench_mgqp.py ;;
+    benchmgqpw) run benchmgqp_wide 600 python tools/bench_mgqp.py --wide ;;
     pmc)
       run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --streams 1
       run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --streams 1
