@@ -232,6 +232,10 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
 // 1 + (n - iq) / n times.  QPGPU_FLAG_EXACT keeps the serial, bit-exact sums.
 // workspace variant's J sweep: rotation coefficients loaded per chunk of this many rotations
 // with the chunk's J entries (0: per rotation, chunks of 16 J loads)
+// workspace variant's l1 scan: two constraints per lane per pass (1) or one (0)
+#ifndef QPGPU_WAVE_GJR_SCAN2
+#define QPGPU_WAVE_GJR_SCAN2 0
+#endif
 #ifndef QPGPU_WAVE_GJR_COEF
 #define QPGPU_WAVE_GJR_COEF 0
 #endif
@@ -1837,6 +1841,43 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           pre_np = EL(CIb, (ls < n ? ls : n - 1) * m + ig);
           pre_c0 = EL(ci0b, ig);
           from_scan = true;
+        }
+      } else if constexpr (GJR && QPGPU_WAVE_GJR_SCAN2) {
+        // workspace variant: a lane's constraints i0 and i0 + S summed together (each in the
+        // reference's j order), so one chunk of CI loads serves both
+        for (int i0 = ls; i0 < m; i0 += 2 * S) {
+          const int i1 = i0 + S;
+          const bool h1 = i1 < m;
+          const int c1i = h1 ? i1 : i0;
+          const double c00 = EL(ci0b, i0), c01 = EL(ci0b, c1i);
+          constexpr int U = 8;
+          double s0 = 0.0, s1 = 0.0;
+          int jb = 0;
+          for (; jb + U <= n; jb += U) {
+            double a0[U], a1[U], xw[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+              a0[u] = EL(CIb, (jb + u) * m + i0);
+              a1[u] = EL(CIb, (jb + u) * m + c1i);
+              xw[u] = xv[jb + u];
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+              s0 += a0[u] * xw[u];
+              s1 += a1[u] * xw[u];
+            }
+          }
+          for (; jb < n; jb++) {
+            const double xj = xv[jb];
+            s0 += EL(CIb, jb * m + i0) * xj;
+            s1 += EL(CIb, jb * m + c1i) * xj;
+          }
+          sv[i0] = s0 + c00;
+          exc[i0] = 0;
+          if (h1) {
+            sv[i1] = s1 + c01;
+            exc[i1] = 0;
+          }
         }
       } else {
         for (int i = ls; i < m; i += S) {
