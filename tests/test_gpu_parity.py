@@ -282,3 +282,16 @@ def test_c4_shard_parity(gpu):
 
     b0, b1 = qpdist.shard(7, 131072)
     assert_parity(qpgpu.make_problems("general", 7, 6, 14, b0, b1, seed=2026), "C4 shard 7")
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_c5_bench_problems_parity(gpu, exact):
+    """The bench's own C5 problems (qpgpu.make_problems, seed 2026: ~134 l1 passes per QP, iq
+    well past 64), so the tolerance-mode loop (tree sums, fused d/z pass, deferred J sweep,
+    DESIGN §5.3) is held to 1e-10 with identical status and pass counts over long active-set
+    paths, and EXACT stays bitwise; QPs from the start and the far end of the batch."""
+    n, p, m = 256, 0, 512
+    for b0 in (0, 4093):
+        pr = qpgpu.make_problems("general", n, p, m, b0, b0 + 3, seed=2026)
+        so, io = assert_parity(pr, f"C5 bench QPs {b0}..{b0 + 2}", exact=exact)
+        assert (so == qpgpu.QP_OK).all() and io.min() > 50, (so, io)
