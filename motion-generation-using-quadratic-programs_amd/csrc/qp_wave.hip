@@ -233,6 +233,10 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
 // workspace variant's J sweep: rotation coefficients loaded per chunk of this many rotations
 // with the chunk's J entries (0: per rotation, chunks of 16 J loads)
 // workspace variant's l1 scan: two constraints per lane per pass (1) or one (0)
+// workspace variant's t1 selection across its four waves (1) or by the lead alone (0)
+#ifndef QPGPU_WAVE_GJR_T1
+#define QPGPU_WAVE_GJR_T1 0
+#endif
 #ifndef QPGPU_WAVE_GJR_SCAN2
 #define QPGPU_WAVE_GJR_SCAN2 0
 #endif
@@ -2017,6 +2021,29 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         }
       sg_argmin<S>(t1best, kbest);
     }
+    // workspace variant: the same selection over its four waves (each wave's butterfly argmin,
+    // then the lead takes the four in order, smaller index on ties): the first minimum of the
+    // reference's sequential scan, with the same divisions
+    constexpr bool kGjrSel = GJR && QPGPU_WAVE_GJR_T1 && S == 4 * 64;
+    if constexpr (kGjrSel) {
+      __syncthreads();  // r from update_r (wave 0 alone)
+      const int iq = ctl->iq;
+      for (int k = p + ls; k < iq; k += S)
+        if (rv[k] > 0.0) {
+          const double q = uv[k] / rv[k];
+          if (q < t1best) {
+            t1best = q;
+            kbest = k;
+          }
+        }
+      sg_argmin<64>(t1best, kbest);
+      double* const W = Q + Ly.off_tsc;
+      if ((ls & 63) == 0) {
+        W[ls >> 6] = t1best;
+        W[4 + (ls >> 6)] = (double)kbest;
+      }
+      __syncthreads();
+    }
     if (lead) {
       const int iq = ctl->iq;
       int l = 0;
@@ -2025,6 +2052,22 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         if (kbest != INT_MAX) {
           t1 = t1best;
           l = Av[kbest];
+        }
+      } else if constexpr (kGjrSel) {
+        const double* const W = Q + Ly.off_tsc;
+        double tb = inf;
+        int kb = INT_MAX;
+        for (int w = 0; w < 4; w++) {
+          const double v = W[w];
+          const int k = (int)W[4 + w];
+          if (v < tb || (v == tb && k < kb)) {
+            tb = v;
+            kb = k;
+          }
+        }
+        if (kb != INT_MAX) {
+          t1 = tb;
+          l = Av[kb];
         }
       } else {
         for (int k = p; k < iq; k++)
