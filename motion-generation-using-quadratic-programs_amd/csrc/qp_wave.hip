@@ -386,7 +386,10 @@ struct WaveCfg {
 // algorithm only ever shifts as zeros), the compute_d transpose scratch [n][kCHS], the loop's
 // vectors, and x z d last — during the setup the factor L ([n][js], rows stride js) overlays
 // everything before x, which is dead until the loop.
-constexpr int kTolCh = 16;  // columns per tree-summed chunk of the tolerance-mode d/z pass
+#ifndef QPGPU_WAVE_TOLCH
+#define QPGPU_WAVE_TOLCH 16
+#endif
+constexpr int kTolCh = QPGPU_WAVE_TOLCH;  // columns per tree-summed chunk of the tolerance-mode d/z pass
 constexpr int kCH = 8, kCHS = kCH + 1;  // compute_d columns per transpose chunk, scratch row stride
 struct WaveLay {
   int js, nr, off_r, off_sc, off_x, off_z, off_d, off_np, off_rv, off_xo, off_gc, off_u, off_uo, off_s,
@@ -909,7 +912,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       grp_sync<S>();
     } else {
       if constexpr (GJR && (QPGPU_WAVE_TOLLOOP & 1) && S == 4 * 64 && NMAX <= S) {
-        if (pre && n >= 2 * 16) {
+        if (pre && n >= 2 * kTolCh) {  // the same test as add_constraint's defer
           // tolerance mode: lane r holds row r of each chunk of kDC columns (column-major J:
           // coalesced), d[c] = sum_r J[r][c] np[r] as per-wave tree sums + the four wave partials
           // in wave order (LDS, double-buffered), then z[r] += J[r][c] d[c] for c >= iq from the
