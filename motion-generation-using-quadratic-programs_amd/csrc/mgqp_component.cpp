@@ -23,16 +23,16 @@ MotionGenerationQuadraticProgram::MotionGenerationQuadraticProgram(const std::st
       in_inertia_port("in_inertia_port"),
       in_robotstatus_port("in_robotstatus_port"),
       out_torques_port("out_torques_port"),
-      out_jointPosLimitInf_port("out_jointPosLimitInf"),
-      out_jointPosLimitSup_port("out_jointPosLimitSup"),
-      out_jointVelLimitInf_port("out_jointVelLimitInf"),
-      out_jointVelLimitSup_port("out_jointVelLimitSup"),
-      out_jointAccLimitInf_port("out_jointAccLimitInf"),
-      out_jointAccLimitSup_port("out_jointAccLimitSup"),
-      out_jointAccDynLimitInf_port("out_jointAccDynLimitInf"),
-      out_jointAccDynLimitSup_port("out_jointAccDynLimitSup"),
-      out_jointTorqueLimitInf_port("out_jointTorqueLimitInf"),
-      out_jointTorqueLimitSup_port("out_jointTorqueLimitSup") {
+      out_jointPosLimitInf_port("out_jointPosLimitInf_port"),
+      out_jointPosLimitSup_port("out_jointPosLimitSup_port"),
+      out_jointVelLimitInf_port("out_jointVelLimitInf_port"),
+      out_jointVelLimitSup_port("out_jointVelLimitSup_port"),
+      out_jointAccLimitInf_port("out_jointAccLimitInf_port"),
+      out_jointAccLimitSup_port("out_jointAccLimitSup_port"),
+      out_jointAccDynLimitInf_port("out_jointAccDynLimitInf_port"),
+      out_jointAccDynLimitSup_port("out_jointAccDynLimitSup_port"),
+      out_jointTorqueLimitInf_port("out_jointTorqueLimitInf_port"),
+      out_jointTorqueLimitSup_port("out_jointTorqueLimitSup_port") {
   // src/mgqp.cpp:89-95
   addOperation("setDOFsize", &MotionGenerationQuadraticProgram::setDOFsize, this, RTT::ClientThread)
       .doc("set DOF size");
@@ -89,6 +89,11 @@ void MotionGenerationQuadraticProgram::removeJointPorts() {
 // src/mgqp.cpp:180-482: (re)creates every port; the per-joint ones are named with suffix 1..DOF
 void MotionGenerationQuadraticProgram::setDOFsize(unsigned int DOFsize) {
   if (portsPrepared_) {
+    // The reference removes the 10 limit ports by names without the "_port" suffix
+    // (src/mgqp.cpp:187-196) although it registers them with it (:412-469), so those 10 are
+    // never removed: kept as is (DESIGN Appendix A).  Re-adding them below replaces the map
+    // entries with the same member ports, as RTT's addPort does for an existing name, and
+    // their connections survive the second setDOFsize.
     for (const char* s : {"in_robotstatus_port", "out_torques_port", "out_jointPosLimitInf",
                           "out_jointPosLimitSup", "out_jointVelLimitInf", "out_jointVelLimitSup",
                           "out_jointAccLimitInf", "out_jointAccLimitSup", "out_jointAccDynLimitInf",

@@ -230,19 +230,9 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
 // sum per row (no serial chain, no LDS round trip) and compute_d + update_z fused into one pass
 // over J (lane = row, column chunks tree-reduced), so J is read once per step instead of
 // 1 + (n - iq) / n times.  QPGPU_FLAG_EXACT keeps the serial, bit-exact sums.
-// workspace variant's J sweep: rotation coefficients loaded per chunk of this many rotations
-// with the chunk's J entries (0: per rotation, chunks of 16 J loads)
-// workspace variant's l1 scan: two constraints per lane per pass (1) or one (0)
-// workspace variant's t1 selection across its four waves (1) or by the lead alone (0)
-#ifndef QPGPU_WAVE_GJR_T1
-#define QPGPU_WAVE_GJR_T1 0
-#endif
-#ifndef QPGPU_WAVE_GJR_SCAN2
-#define QPGPU_WAVE_GJR_SCAN2 0
-#endif
-#ifndef QPGPU_WAVE_GJR_COEF
-#define QPGPU_WAVE_GJR_COEF 0
-#endif
+// (Variants measured neutral or slower on C5 and removed in round 3, kept in git history:
+// coefficients loaded per chunk of rotations in the J sweep, two constraints per lane in the
+// l1 scan, the t1 selection across the four waves — DESIGN §5.3.)
 #ifndef QPGPU_WAVE_TOLLOOP
 #define QPGPU_WAVE_TOLLOOP 7  // bit 0: fused compute_d + update_z, bit 1: tree update_r,
                               // bit 2: add_constraint J sweep deferred into the next d/z pass
@@ -278,31 +268,16 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 // J = L^{-T} by column-oriented forward substitution, and cholesky_solve runs across the lanes
 // with v_readlane broadcasts.  Every element sees the reference's operations in the reference's
 // order (see the block), so results are bitwise unchanged.
-// CI columns kept in registers across the active-set loop (one-wave-per-SIMD variant): measured
-// slower (C3 16.7 vs 15.4 ms, profiles/r02_s8: the 128 extra live VGPRs cost the loop's other
-// phases AGPR copies and scratch), so off; the scan instead issues all of a lane's CI loads at
-// once (kScanWide)
-// l1 scan with all of a lane's CI loads issued at once (buffer loads): measured slower (C3
-// 16.0 vs 15.3 ms, scan 196k vs 144k cycles per block, profiles/r02_s10): off
+// (Removed in round 3 after measuring slower, kept in git history: CI columns in registers
+// across the loop — C3 16.7 vs 15.4 ms, profiles/r02_s8 —, all of a lane's CI loads issued at
+// once in the scan — 16.0 vs 15.3 ms, profiles/r02_s10 —, and J in registers with packed R at
+// two waves per SIMD — C3 18.7 vs 14.5 ms, mgqp 1.96 vs 1.76 ms, profiles/r02_s19.)
 // four QPs per wave (S = 16) for n <= 16, m <= 32 (the mgqp hierarchy levels)
 #ifndef QPGPU_WAVE_S16
 #define QPGPU_WAVE_S16 1
 #endif
 #ifndef QPGPU_WAVE_FALLTHRU
 #define QPGPU_WAVE_FALLTHRU 1
-#endif
-#ifndef QPGPU_WAVE_SCANWIDE
-#define QPGPU_WAVE_SCANWIDE 0
-#endif
-#ifndef QPGPU_WAVE_CIREG
-#define QPGPU_WAVE_CIREG 0
-#endif
-// J in registers (one row per lane) with packed R and compute_d through an LDS transpose, for
-// two waves per SIMD: correct (parity green) but measured slower (profiles/r02_s19: C3 18.7 vs
-// 14.5 ms — the S = 32 kernel spills at 256 VGPRs — and mgqp 1.96 vs 1.76 ms — the transposed
-// compute_d doubles d/z), so off
-#ifndef QPGPU_WAVE_REGJ
-#define QPGPU_WAVE_REGJ 0
 #endif
 #ifndef QPGPU_WAVE_RPACK
 #define QPGPU_WAVE_RPACK 1
@@ -348,6 +323,9 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 // diagnostic stamps only: slots 5..7 hold, instead of the equality-phase parts, the loop's
 // update_r cycles, step count and sum of iq over steps (1), or add_constraint's |h| chain +
 // coefficients, J sweep and R column + test cycles, equality phase and loop together (2)
+#ifndef QPGPU_WAVE_GJR_CAP
+#define QPGPU_WAVE_GJR_CAP 0
+#endif
 #ifndef QPGPU_WAVE_STAMPS_DETAIL
 #define QPGPU_WAVE_STAMPS_DETAIL 0
 #endif
@@ -380,30 +358,22 @@ struct WaveCfg {
 // Vectors: x z d np r x_old (n each), the Givens coefficients (4n, interleaved per rotation),
 // u u_old (n+1 each), s (m), then int A A_old
 // (n+1 each), uint8 act exc (m each) and the control block.
-//
-// REGJ layout (J in registers, one row per lane; see kRegJ): R packed (upper triangle row by row,
-// then the first subdiagonal, then one write-only slot for the entries below it, which the
-// algorithm only ever shifts as zeros), the compute_d transpose scratch [n][kCHS], the loop's
-// vectors, and x z d last — during the setup the factor L ([n][js], rows stride js) overlays
-// everything before x, which is dead until the loop.
 #ifndef QPGPU_WAVE_TOLCH
 #define QPGPU_WAVE_TOLCH 16
 #endif
 constexpr int kTolCh = QPGPU_WAVE_TOLCH;  // columns per tree-summed chunk of the tolerance-mode d/z pass
-constexpr int kCH = 8, kCHS = kCH + 1;  // compute_d columns per transpose chunk, scratch row stride
 struct WaveLay {
-  int js, nr, off_r, off_sc, off_x, off_z, off_d, off_np, off_rv, off_xo, off_gc, off_u, off_uo, off_s,
+  int js, nr, off_r, off_x, off_z, off_d, off_np, off_rv, off_xo, off_gc, off_u, off_uo, off_s,
       off_a, off_fl, off_ctl, off_tsc, stride;
 };
-__host__ __device__ inline WaveLay wave_lay(int n, int m, bool gjr, bool regj = false, bool rpack = false) {
+__host__ __device__ inline WaveLay wave_lay(int n, int m, bool gjr, bool rpack = false) {
   WaveLay L;
   L.js = (n + 1) | 1;
   L.nr = n * (n + 1) / 2 + (n > 0 ? n - 1 : 0) + 1;
-  if (rpack && !regj && !gjr) {
+  if (rpack && !gjr) {
     // J [n][js] at 0, R packed after it, the loop's vectors, then x z d; during the setup the
     // factor L ([n][js]) overlays R and the loop's vectors
     L.off_r = n * L.js;
-    L.off_sc = L.off_r;
     L.off_np = L.off_r + L.nr;
     L.off_rv = L.off_np + n;
     L.off_xo = L.off_rv + n;
@@ -418,9 +388,8 @@ __host__ __device__ inline WaveLay wave_lay(int n, int m, bool gjr, bool regj = 
     L.off_z = L.off_x + n;
     L.off_d = L.off_z + n;
     L.off_ctl = L.off_d + n;
-  } else if (!regj) {
+  } else {
     L.off_r = gjr ? 0 : n * L.js;
-    L.off_sc = L.off_r;
     L.off_x = gjr ? 0 : 2 * n * L.js;
     L.off_z = L.off_x + n;
     L.off_d = L.off_z + n;
@@ -434,30 +403,14 @@ __host__ __device__ inline WaveLay wave_lay(int n, int m, bool gjr, bool regj = 
     L.off_a = L.off_s + m;
     L.off_fl = L.off_a + (2 * (n + 1) + 1) / 2;
     L.off_ctl = L.off_fl + (2 * m + 7) / 8;
-  } else {
-    L.off_r = 0;
-    L.off_sc = L.nr;
-    L.off_np = L.off_sc + n * kCHS;
-    L.off_rv = L.off_np + n;
-    L.off_xo = L.off_rv + n;
-    L.off_gc = L.off_xo + n;
-    L.off_u = L.off_gc + 4 * n;
-    L.off_uo = L.off_u + n + 1;
-    L.off_s = L.off_uo + n + 1;
-    L.off_a = L.off_s + m;
-    L.off_fl = L.off_a + (2 * (n + 1) + 1) / 2;
-    const int end = L.off_fl + (2 * m + 7) / 8;
-    L.off_x = end > n * L.js ? end : n * L.js;
-    L.off_z = L.off_x + n;
-    L.off_d = L.off_z + n;
-    L.off_ctl = L.off_d + n;
   }
   // the workspace variant's tolerance-mode partial sums (two buffers of 4 waves x kTolCh)
   L.off_tsc = L.off_ctl + (int)((sizeof(Ctl) + 7) / 8);
   L.stride = (L.off_tsc + (gjr ? 2 * 4 * kTolCh : 0)) | 1;
   return L;
 }
-// packed-R index (REGJ): R[i][j] for j >= i, the subdiagonal R[j+1][j], else the write-only slot
+// packed-R index: R[i][j] for j >= i, the subdiagonal R[j+1][j], else a write-only slot (the
+// entries below it, which the algorithm only ever shifts as zeros)
 __device__ __forceinline__ int rpk(int i, int j, int n) {
   const int nup = n * (n + 1) / 2;
   return j >= i ? i * n - (i * (i - 1)) / 2 + (j - i) : (i == j + 1 ? nup + j : nup + n - 1);
@@ -472,29 +425,19 @@ template <int S, int NMAX, int MMAX, bool GJR, int OCC = 1>
 __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
     qp_wave_kernel(const QpArgs a, double* __restrict__ ws) {
   using C = WaveCfg<S, NMAX, MMAX, GJR>;
-  // J in registers (lane r holds row r) and R packed, so a two-QP block of C3 fits 20 KiB of LDS
-  // and two waves run on every SIMD (launched at OCC = 2)
-  constexpr bool kRegJ = QPGPU_WAVE_REGJ && !GJR && S <= 32 && NMAX <= S && OCC == 2;
   constexpr bool kRegSetup = QPGPU_WAVE_REGSETUP && !GJR && NMAX <= S &&
-                             ((S == 32 && OCC == 1) || (S == 16 && OCC <= 2) || kRegJ);
+                             ((S == 32 && OCC == 1) || (S == 16 && OCC <= 2));
   // R packed (upper triangle + subdiagonal) with J still in LDS: less LDS per QP, more resident
   // blocks per CU (the register setup keeps the factor L in its own overlay)
-  constexpr bool kRPack = QPGPU_WAVE_RPACK && kRegSetup && !kRegJ;
-  constexpr bool kPackedR = kRegJ || kRPack;
+  constexpr bool kRPack = QPGPU_WAVE_RPACK && kRegSetup;
+  constexpr bool kPackedR = kRPack;
   // lane-parallel selections (argmin of s for l2, of u/r for t1) for one-wave subgroups
   constexpr bool kLaneSel = S <= 64;
-  // the one-wave-per-SIMD variant keeps each lane's CI columns (and ci0) in registers from the
-  // first l1 scan on
-  constexpr bool kCiReg = QPGPU_WAVE_CIREG && kRegSetup && MMAX <= 64 && MMAX % S == 0;
-  constexpr int kCU = kCiReg ? MMAX / S : 1;
-  // l1 scan with every CI load of a lane in flight at once (<= 2 constraints per lane)
-  constexpr bool kScanWide = QPGPU_WAVE_SCANWIDE && !kCiReg && kRegSetup && MMAX <= 2 * S;
-  constexpr int kWU = (MMAX + S - 1) / S;
   // loads in flight per lane in the global-operand sums (deeper for the one-QP-per-workgroup
   // workspace variant, whose lanes have registers to spare)
   constexpr int KG = GJR ? 16 : kUG;
   extern __shared__ double lds[];
-  const WaveLay Ly = wave_lay(a.n, a.m, GJR, kRegJ, kRPack);
+  const WaveLay Ly = wave_lay(a.n, a.m, GJR, kRPack);
   const int JS = GJR ? BigWs<NMAX>::JS : Ly.js;
 
   const int tid = threadIdx.x;
@@ -507,8 +450,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   double* const Q = lds + sg * Ly.stride;
   double* const Jm = GJR ? ws + (b < a.batch ? b : 0) * (int64_t)C::WS_DOUBLES : Q;
   double* const Rm = GJR ? Jm + BigWs<NMAX>::OFF_R : Q + Ly.off_r;
-  double* const Lm = kRegJ ? Q : Rm;  // the factor L during the setup ([n][js])
-  [[maybe_unused]] double* const sc = Q + Ly.off_sc;  // compute_d transpose scratch (REGJ)
+  double* const Lm = Rm;  // the factor L during the setup ([n][js])
   const int nv = a.n;
   double* const xv = Q + Ly.off_x;
   double* const zv = Q + Ly.off_z;
@@ -547,8 +489,6 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
 #define J_(i, j) (GJR ? Jm[(j) * JS + (i)] : Jm[(i) * JS + (j)])
 #define R_(i, j) Rm[kPackedR ? rpk((i), (j), n) : (i) * JS + (j)]
 #define L_(i, j) Lm[(i) * JS + (j)]
-  // J in registers (kRegJ): lane r holds row r, indexed with compile-time column indices only
-  [[maybe_unused]] double Jr[kRegJ ? NMAX : 1];
   // setup already in the workspace (qp_panel.hip): start from its header
   const bool pre = GJR && (a.flags & kSetupDone);
 
@@ -712,28 +652,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       double w[NMAX];
 #pragma unroll
       for (int k = 0; k < NMAX; k++) w[k] = (k == j) ? 1.0 : 0.0;
-      if constexpr (kRegJ) {
-        // J stays in registers: the outputs shift through Jr as well, so after NMAX steps (those
-        // past n only touch entries past n, which end as +0.0) Jr[k] = y_k at compile-time k
-#pragma unroll 1
-        for (int q = 0; q < NMAX; q++) {
-          const int qc = q < n ? q : n - 1;
-          const double* Lq = Lm + qc * JS + qc;
-          const double y = w[0] / Lq[0];
-#pragma unroll
-          for (int k = 0; k + 1 < NMAX; k++) Jr[k] = Jr[k + 1];
-          Jr[NMAX - 1] = y;
-#pragma unroll
-          for (int k = 0; k + 1 < NMAX; k++) w[k] = w[k + 1] - Lq[k + 1] * y;
-          w[NMAX - 1] = 0.0;
-        }
-#pragma unroll
-        for (int k = 0; k < NMAX; k++) Jr[k] = (mine && k < n) ? Jr[k] : 0.0;
-        double dj = 0.0;  // J[j][j], for c2 = trace(J)
-#pragma unroll
-        for (int k = 0; k < NMAX; k++) dj = (k == j) ? Jr[k] : dj;
-        if (mine) dv[j] = dj;
-      } else {
+      {
         for (int q = 0; q < n; q++) {
           const double* Lq = Lm + q * JS + q;  // Lq[k] = L[q+k][q] (k >= 1), Lq[0] = L[q][q]
           double lc[NMAX];
@@ -780,7 +699,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       grp_sync<S>();
       if (lead) {
         double c2 = 0.0;
-        for (int i = 0; i < n; i++) c2 += kRegJ ? dv[i] : J_(i, i);
+        for (int i = 0; i < n; i++) c2 += J_(i, i);
         ctl->c2 = c2;
         double f = 0.0;
         for (int i = 0; i < n; i++) f += zv[i] * xv[i];
@@ -867,50 +786,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   int pend = -1;
   constexpr bool kDefer = GJR && (QPGPU_WAVE_TOLLOOP & 4) && (QPGPU_WAVE_TOLLOOP & 1) && S == 4 * 64 && NMAX <= S;
   auto compute_d_z = [&](int iq) {
-    if constexpr (kRegJ) {
-      // d[c] = sum_j J[j][c] np[j] (j ascending) with row j in lane j's registers: the products
-      // J[j][c] np[j] (the reference's roundings) go through the scratch kCH columns at a time,
-      // and lane c adds column c's n products in row order
-      const double npr = ls < n ? npv[ls] : 0.0;
-#pragma unroll
-      for (int c0 = 0; c0 < NMAX; c0 += kCH) {
-        if (c0 < n) {
-          if (ls < n)
-#pragma unroll
-            for (int u = 0; u < kCH; u++)
-              if (c0 + u < NMAX) sc[ls * kCHS + u] = Jr[c0 + u < NMAX ? c0 + u : 0] * npr;
-          grp_sync<S>();
-          const int c = ls - c0;
-          if (c >= 0 && c < kCH && ls < n) {
-            double sd = 0.0;
-            constexpr int U = 8;
-            for (int jb = 0; jb < n; jb += U) {
-              double pv[U];
-#pragma unroll
-              for (int u = 0; u < U; u++) pv[u] = jb + u < n ? sc[(jb + u) * kCHS + c] : 0.0;
-#pragma unroll
-              for (int u = 0; u < U; u++)
-                if (jb + u < n) sd += pv[u];
-            }
-            dv[ls] = sd;
-          }
-          grp_sync<S>();
-        }
-      }
-      // z[r] = sum_{j >= iq} J[r][j] d[j] (j ascending) in lane r's registers; entries below iq
-      // or past n add +0.0 to a sum that starts at +0.0 (never -0.0): no-ops
-      if (ls < n) {
-        double z = 0.0;
-#pragma unroll
-        for (int j = 0; j < NMAX; j++) {
-          const double dj = dv[j < n ? j : 0];
-          z += (j >= iq && j < n) ? Jr[j] * dj : 0.0;
-          if (j % 8 == 7) __builtin_amdgcn_sched_barrier(0);  // d loads 8 at a time (registers)
-        }
-        zv[ls] = z;
-      }
-      grp_sync<S>();
-    } else {
+    {
       if constexpr (GJR && (QPGPU_WAVE_TOLLOOP & 1) && S == 4 * 64 && NMAX <= S) {
         if (pre && n >= 2 * kTolCh) {  // the same test as add_constraint's defer
           // tolerance mode: lane r holds row r of each chunk of kDC columns (column-major J:
@@ -1333,8 +1209,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       // Row k's sweep over columns n-1 .. iq: rotation g maps (J[k][j-1], J[k][j]), j = n-1-g,
       // to (n1, xny (t1 + n1) - t2) and n1 is the next rotation's t2, so it is carried in a
       // register and the t1 loads (independent of the chain) are issued kU at a time.
-      constexpr bool kGC = GJR && QPGPU_WAVE_GJR_COEF;  // workspace variant, coefficients per chunk
-      constexpr int kU = GJR ? (kGC ? QPGPU_WAVE_GJR_COEF : KG) : QPGPU_WAVE_KUJ;
+      constexpr bool kGC = false;  // (coefficients per chunk in the workspace variant: removed)
+      constexpr int kU = GJR ? KG : QPGPU_WAVE_KUJ;
       const int ng = ctl->ngiv;
       for (int k = ls; k < n; k += S) {
         double carry = J_(k, n - 1);
@@ -1379,25 +1255,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         J_(k, n - 1 - ng) = carry;
       }
     };
-    if (kRegJ && iq0 < n) {
-      // the same sweep on lane k's register row: rotation g = n-1-j on columns (j-1, j), j from
-      // n-1 down to iq+1, with the reference's operations; out-of-range steps leave both columns
-      if (ls < n) {
-#pragma unroll
-        for (int j = NMAX - 1; j >= 1; j--) {
-          const int g = n - 1 - j;
-          const bool on = j <= n - 1 && j >= iq0 + 1;
-          const int gi = on ? g : 0;
-          const double c = GC_(gi), sn = GS_(gi), xn = GX_(gi);
-          const bool f = on && GF_(gi) != 0.0;
-          const double t1 = Jr[j - 1], t2 = Jr[j];
-          const double n1 = t1 * c + t2 * sn;
-          Jr[j - 1] = f ? n1 : t1;
-          Jr[j] = f ? xn * (t1 + n1) - t2 : t2;
-          if (j % 4 == 0) __builtin_amdgcn_sched_barrier(0);  // coefficients 4 steps at a time
-        }
-      }
-    } else if (!GJR && QPGPU_WAVE_SWEEP2 && iq0 < n) {
+    if (!GJR && QPGPU_WAVE_SWEEP2 && iq0 < n) {
       // the sweep below with J in LDS: full chunks of kU rotations with no per-rotation
       // exec-mask branch (the chunk's J entries and coefficients loaded first), then the tail
       // one rotation per trip
@@ -1544,25 +1402,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       // to (n1, xny (n1 + t1) - t2); the second is the next rotation's t1 (carried)
       constexpr int kU = GJR ? KG : QPGPU_WAVE_KUJ;
       const int ng = ctl->ngiv, qq = ctl->qq;
-      if constexpr (kRegJ) {
-        // lane k's register row: rotation g = j - qq on columns (j, j+1), j ascending
-        if (ls < n) {
-#pragma unroll
-          for (int j = 0; j + 1 < NMAX; j++) {
-            const int g = j - qq;
-            const bool on = g >= 0 && g < ng;
-            const int gi = on ? g : 0;
-            const double c = GC_(gi), sn = GS_(gi), xn = GX_(gi);
-            const bool f = on && GF_(gi) != 0.0;
-            const double t1 = Jr[j], t2 = Jr[j + 1];
-            const double n1 = t1 * c + t2 * sn;
-            Jr[j] = f ? n1 : t1;
-            Jr[j + 1] = f ? xn * (n1 + t1) - t2 : t2;
-            if (j % 4 == 3) __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-      }
-      for (int k = kRegJ ? n : ls; k < n; k += S) {
+      for (int k = ls; k < n; k += S) {
         double carry = J_(k, qq);
         for (int gb = 0; gb < ng; gb += kU) {
           constexpr int kUC = GJR ? 1 : kU;
@@ -1674,8 +1514,6 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   // ------------------------------------------------------------------ active-set loop
   // Per-subgroup state machine; a wave loops until all of its QPs are done.
   const int max_steps = a.max_steps;
-  [[maybe_unused]] double cir[kCU][kCiReg ? NMAX : 1], c0r[kCU];
-  [[maybe_unused]] bool ci_in_regs = false;
   // the select that follows a scan (carried ss reset to 0): its argmin, the np gather and
   // ci0[ip] are started inside the scan, so their global loads overlap the lead's psi sum
   constexpr bool kPreSel = QPGPU_WAVE_PRESEL && kLaneSel && !GJR && MMAX <= 2 * S && NMAX <= S;
@@ -1708,75 +1546,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           uo[i] = uv[i];
         }
       }
-      if constexpr (kCiReg) {
-        // columns ls + u*S of CI (and ci0) stay in registers after the first scan; entries past
-        // n are +0.0 against x = +0.0, and adding +0.0 leaves every partial sum unchanged (a
-        // running sum from +0.0 is never -0.0)
-        if (!ci_in_regs) {
-          const int64_t rs = (int64_t)m * T;  // element stride between CI rows
-#pragma unroll
-          for (int u = 0; u < kCU; u++) {
-            const int i = ls + u * S;
-            const double* cb = CIb + (int64_t)(i < m ? i : 0) * T;
-#pragma unroll
-            for (int j = 0; j < NMAX; j++) cir[u][j] = (i < m && j < n) ? cb[j * rs] : 0.0;
-            c0r[u] = i < m ? EL(ci0b, i) : 0.0;
-          }
-          ci_in_regs = true;
-        }
-#pragma unroll
-        for (int u = 0; u < kCU; u++) {
-          const int i = ls + u * S;
-          double s = 0.0;
-#pragma unroll
-          for (int j = 0; j < NMAX; j++) s += cir[u][j] * (j < n ? xv[j] : 0.0);
-          s += c0r[u];
-          if (i < m) {
-            sv[i] = s;
-            exc[i] = 0;
-          }
-        }
-      } else if constexpr (kScanWide) {
-        // all of this lane's CI column loads issued before the first multiply-add (one memory
-        // latency per scan); entries past n are +0.0 against x = +0.0 (no-op adds, see above)
-        // buffer loads off the wave's first QP (uniform descriptor): one offset VGPR per lane,
-        // the row stride in the scalar offset
-        const int64_t wb0 = (int64_t)blockIdx.x * C::QPB;
-        const double* ciw = a.CI + qbase_rt(wb0, n * m, T);
-        const uint64_t cp = reinterpret_cast<uint64_t>(ciw);
-        // readfirstlane returns int: keep both halves unsigned (no sign extension into the high
-        // word) so the descriptor's base is the pointer
-        const uint32_t cp_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cp);
-        const uint32_t cp_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cp >> 32));
-        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<void*>(((uint64_t)cp_hi << 32) | cp_lo), 0, 0x7fffffff, 0x00020000);
-        const int qoff = live ? (int)(qbase_rt(bb, n * m, T) - qbase_rt(wb0, n * m, T)) : 0;
-        double cw[kWU][NMAX], c0w[kWU];
-#pragma unroll
-        for (int u = 0; u < kWU; u++) {
-          const int i = ls + u * S;
-          const int vo = (qoff + (i < m ? i : 0) * T) * 8;
-#pragma unroll
-          for (int j = 0; j < NMAX; j++)
-            cw[u][j] = (i < m && j < n)
-                           ? __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
-                                                            rsrc, vo, (j < n ? j : 0) * m * T * 8, 0))
-                           : 0.0;
-          c0w[u] = i < m ? EL(ci0b, i) : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < kWU; u++) {
-          const int i = ls + u * S;
-          double s = 0.0;
-#pragma unroll
-          for (int j = 0; j < NMAX; j++) s += cw[u][j] * (j < n ? xv[j] : 0.0);
-          s += c0w[u];
-          if (i < m) {
-            sv[i] = s;
-            exc[i] = 0;
-          }
-        }
-      } else if constexpr (!GJR && MMAX <= 2 * S) {
+      if constexpr (!GJR && MMAX <= 2 * S) {
         // a lane's two constraints (i0 = ls, i1 = ls + S) summed together, so each chunk of CI
         // loads covers both and a scan waits on half as many memory latencies; each sum keeps the
         // reference's j order (the second constraint's index is clamped when it does not exist,
@@ -1848,43 +1618,6 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           pre_np = EL(CIb, (ls < n ? ls : n - 1) * m + ig);
           pre_c0 = EL(ci0b, ig);
           from_scan = true;
-        }
-      } else if constexpr (GJR && QPGPU_WAVE_GJR_SCAN2) {
-        // workspace variant: a lane's constraints i0 and i0 + S summed together (each in the
-        // reference's j order), so one chunk of CI loads serves both
-        for (int i0 = ls; i0 < m; i0 += 2 * S) {
-          const int i1 = i0 + S;
-          const bool h1 = i1 < m;
-          const int c1i = h1 ? i1 : i0;
-          const double c00 = EL(ci0b, i0), c01 = EL(ci0b, c1i);
-          constexpr int U = 8;
-          double s0 = 0.0, s1 = 0.0;
-          int jb = 0;
-          for (; jb + U <= n; jb += U) {
-            double a0[U], a1[U], xw[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-              a0[u] = EL(CIb, (jb + u) * m + i0);
-              a1[u] = EL(CIb, (jb + u) * m + c1i);
-              xw[u] = xv[jb + u];
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-              s0 += a0[u] * xw[u];
-              s1 += a1[u] * xw[u];
-            }
-          }
-          for (; jb < n; jb++) {
-            const double xj = xv[jb];
-            s0 += EL(CIb, jb * m + i0) * xj;
-            s1 += EL(CIb, jb * m + c1i) * xj;
-          }
-          sv[i0] = s0 + c00;
-          exc[i0] = 0;
-          if (h1) {
-            sv[i1] = s1 + c01;
-            exc[i1] = 0;
-          }
         }
       } else {
         for (int i = ls; i < m; i += S) {
@@ -2024,29 +1757,6 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         }
       sg_argmin<S>(t1best, kbest);
     }
-    // workspace variant: the same selection over its four waves (each wave's butterfly argmin,
-    // then the lead takes the four in order, smaller index on ties): the first minimum of the
-    // reference's sequential scan, with the same divisions
-    constexpr bool kGjrSel = GJR && QPGPU_WAVE_GJR_T1 && S == 4 * 64;
-    if constexpr (kGjrSel) {
-      __syncthreads();  // r from update_r (wave 0 alone)
-      const int iq = ctl->iq;
-      for (int k = p + ls; k < iq; k += S)
-        if (rv[k] > 0.0) {
-          const double q = uv[k] / rv[k];
-          if (q < t1best) {
-            t1best = q;
-            kbest = k;
-          }
-        }
-      sg_argmin<64>(t1best, kbest);
-      double* const W = Q + Ly.off_tsc;
-      if ((ls & 63) == 0) {
-        W[ls >> 6] = t1best;
-        W[4 + (ls >> 6)] = (double)kbest;
-      }
-      __syncthreads();
-    }
     if (lead) {
       const int iq = ctl->iq;
       int l = 0;
@@ -2055,22 +1765,6 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         if (kbest != INT_MAX) {
           t1 = t1best;
           l = Av[kbest];
-        }
-      } else if constexpr (kGjrSel) {
-        const double* const W = Q + Ly.off_tsc;
-        double tb = inf;
-        int kb = INT_MAX;
-        for (int w = 0; w < 4; w++) {
-          const double v = W[w];
-          const int k = (int)W[4 + w];
-          if (v < tb || (v == tb && k < kb)) {
-            tb = v;
-            kb = k;
-          }
-        }
-        if (kb != INT_MAX) {
-          t1 = tb;
-          l = Av[kb];
         }
       } else {
         for (int k = p; k < iq; k++)
@@ -2210,14 +1904,6 @@ template <int S, int NMAX, int MMAX, bool GJR>
 static hipError_t launch_wave(const QpArgs& a, hipStream_t stream, double* ws) {
   using C = WaveCfg<S, NMAX, MMAX, GJR>;
   const int64_t blocks = (a.batch + C::QPB - 1) / C::QPB;
-  // J in registers (kRegJ): the smaller REGJ layout, two waves per SIMD (C3: 19.8 KiB per
-  // two-QP block, 8 blocks per CU)
-  if constexpr (QPGPU_WAVE_REGJ && S <= 32 && !GJR && NMAX <= S) {
-    const size_t lds_j = (size_t)C::QPB * wave_lay(a.n, a.m, GJR, true).stride * sizeof(double);
-    hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR, 2>), dim3((unsigned)blocks), dim3(C::BS), lds_j,
-                       stream, a, ws);
-    return hipGetLastError();
-  }
   size_t lds_bytes = (size_t)C::QPB * wave_lay(a.n, a.m, GJR).stride * sizeof(double);
   // Two-QP-per-wave variants: when a block's LDS leaves room for >= 2 waves per SIMD (<= 20 KiB,
   // i.e. >= 8 one-wave blocks per CU) register pressure is the occupancy limit, so launch the
@@ -2226,17 +1912,12 @@ static hipError_t launch_wave(const QpArgs& a, hipStream_t stream, double* ws) {
   // keeps the unconstrained allocation (21.0 vs 22.0 ms).  The register-setup instantiations
   // (OCC 2 for S = 16, OCC 1) use the packed-R layout when QPGPU_WAVE_RPACK is on.
   if constexpr (S < 64 && !GJR) {
-    // QPGPU_WAVE_OCC4_LDS (diagnostic) moves the 20 KiB threshold
-    static const size_t occ4_lds = [] {
-      const char* e = getenv("QPGPU_WAVE_OCC4_LDS");
-      return e ? (size_t)atol(e) : (size_t)20480;
-    }();
-    if (lds_bytes <= occ4_lds) {
+    if (lds_bytes <= 20480) {
       hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR, 4>), dim3((unsigned)blocks), dim3(C::BS),
                          lds_bytes, stream, a, ws);
       return hipGetLastError();
     }
-    const size_t lds_p = (size_t)C::QPB * wave_lay(a.n, a.m, GJR, false, QPGPU_WAVE_RPACK != 0).stride * sizeof(double);
+    const size_t lds_p = (size_t)C::QPB * wave_lay(a.n, a.m, GJR, QPGPU_WAVE_RPACK != 0).stride * sizeof(double);
     // four-QP waves (S = 16): up to 40 KiB per block still leaves room for two waves per SIMD
     if (S == 16 && lds_bytes <= 40960) {
       hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR, 2>), dim3((unsigned)blocks), dim3(C::BS),
@@ -2245,19 +1926,13 @@ static hipError_t launch_wave(const QpArgs& a, hipStream_t stream, double* ws) {
     }
     lds_bytes = lds_p;  // OCC 1 (register setup) from here on
   }
-  // workspace variant (n > 64): QPGPU_WAVE_GJR_BLOCKS_PER_CU = k pads the dynamic LDS so at most
-  // k one-QP workgroups share a CU (diagnostic: fewer resident QPs = a working set that stays in
-  // the Infinity Cache; 0 = no cap)
-  if constexpr (GJR) {
-    static int cap = -1;
-    if (cap < 0) {
-      const char* e = getenv("QPGPU_WAVE_GJR_BLOCKS_PER_CU");
-      cap = e ? atoi(e) : 0;
-    }
-    if (cap > 0) {
-      const size_t want = (size_t)163840 / (size_t)cap - 1024;
-      if (want > lds_bytes) lds_bytes = want;
-    }
+  // workspace variant (n > 64): an A/B build with -DQPGPU_WAVE_GJR_CAP=k pads the dynamic LDS so
+  // at most k one-QP workgroups share a CU (fewer resident QPs = a working set that may stay in
+  // the Infinity Cache).  The product build has no cap.
+  if constexpr (GJR && QPGPU_WAVE_GJR_CAP > 0) {
+    constexpr size_t cap = QPGPU_WAVE_GJR_CAP > 0 ? QPGPU_WAVE_GJR_CAP : 1;
+    const size_t want = (size_t)163840 / cap - 1024;
+    if (want > lds_bytes) lds_bytes = want;
   }
   static size_t granted = 0;  // dynamic LDS beyond 64 KiB must be granted per kernel
   if (lds_bytes > 65536 && lds_bytes > granted) {

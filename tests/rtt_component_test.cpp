@@ -208,7 +208,15 @@ int main(int argc, char** argv) {
   // setDOFsize's port set: 3 + 11*DOF inputs, 11 outputs (src/mgqp.cpp:180-482)
   CHECK((int)tc->ports()->getPortNames().size() == 3 + 11 * dof + 11);
   CHECK(tc->ports()->getPort("in_jacobian_port_" + d) != nullptr);
-  CHECK(tc->ports()->getPort("out_jointAccDynLimitSup") != nullptr);
+  // the 10 limit ports by the names the reference registers (src/mgqp.cpp:412-469) and the
+  // OCL reporter subscribes to (ops/logData.ops:17-26)
+  static const char* kLimitPorts[] = {
+      "out_jointPosLimitInf_port",    "out_jointPosLimitSup_port",    "out_jointVelLimitInf_port",
+      "out_jointVelLimitSup_port",    "out_jointAccLimitInf_port",    "out_jointAccLimitSup_port",
+      "out_jointAccDynLimitInf_port", "out_jointAccDynLimitSup_port", "out_jointTorqueLimitInf_port",
+      "out_jointTorqueLimitSup_port"};
+  for (const char* nm : kLimitPorts) CHECK(dynamic_cast<RTT::OutputPort<VecF>*>(tc->ports()->getPort(nm)) != nullptr);
+  CHECK(tc->ports()->getPort("out_jointAccDynLimitSup") == nullptr);
   CHECK(tc->ports()->getPort("in_jacobian_port_" + std::to_string(dof + 1)) == nullptr);
 
   Fkin fkin("fkin7");
@@ -235,8 +243,13 @@ int main(int argc, char** argv) {
   CHECK(!dep.connect("singen.out_sin_port", "myTorqueController.in_h_port", cp));  // type mismatch
   CHECK(!tc->configure());  // out_torques_port still unconnected
   CHECK(dep.connect("myTorqueController.out_torques_port", "robot_gazebo.full_arm_JointTorqueCtrl", cp));
-  RTT::InputPort<VecF> accdyn_sink("accdyn");
-  CHECK(dynamic_cast<RTT::OutputPort<VecF>*>(tc->ports()->getPort("out_jointAccDynLimitInf"))->connectTo(accdyn_sink));
+  // every limit port connected by name, as ops/logData.ops:17-26 reports them
+  std::vector<std::unique_ptr<RTT::InputPort<VecF>>> limit_sinks;
+  for (const char* nm : kLimitPorts) {
+    limit_sinks.emplace_back(new RTT::InputPort<VecF>(std::string("sink_") + nm));
+    CHECK(dynamic_cast<RTT::OutputPort<VecF>*>(tc->ports()->getPort(nm))->connectTo(*limit_sinks.back()));
+  }
+  RTT::InputPort<VecF>& accdyn_sink = *limit_sinks[6];
   CHECK(tc->configure());
   CHECK(tc->start());
 
@@ -296,6 +309,10 @@ int main(int argc, char** argv) {
   CHECK((int)tc->ports()->getPortNames().size() == 3 + 11 * 3 + 11);
   CHECK(tc->ports()->getPort("in_jacobian_port_7") == nullptr);
   CHECK(!dynamic_cast<RTT::InputPort<VecF>*>(tc->ports()->getPort("in_h_port"))->connected());
+  // the reference's removePort names miss the limit ports' "_port" suffix (src/mgqp.cpp:187-196
+  // vs :412-469): they are not removed, so their connections survive (kept defect)
+  for (const char* nm : kLimitPorts) CHECK(tc->ports()->getPort(nm) != nullptr);
+  CHECK(dynamic_cast<RTT::OutputPort<VecF>*>(tc->ports()->getPort("out_jointAccDynLimitInf_port"))->connected());
 
   // a throwing solve puts the component in the Exception state, like an exception escaping
   // RTT's updateHook: the task joint's jacobian has three identical rows, so level 0's

@@ -15,7 +15,7 @@ for f in qp_layout qp_lane qp_small qp_wave qp_panel qpgpu_api; do [ "$f" = "$SR
 (cd "$OUT/tmp" && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-fast-math -fPIC \
    -std=c++17 -I"$ROOT/include" "$@" -c "$PKG/csrc/$SRC.hip" -o "$OUT/$SRC.o" -save-temps 2>&1 | grep -v warning | grep -v "warnings\? generated" || true)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libqpgpu.so" "$OUT"/*.o
-if [ "$SRC" = qp_lane ]; then PAT=qp_lane_kernelILi7ELi14ELi1ELb1ELi64; else PAT=${SRC}_kernel; fi
+if [ "$SRC" = qp_lane ]; then PAT=qp_lane_kernelILi7ELi14ELi1ELb1ELi6; else PAT=${SRC}_kernel; fi
 python3 "$ROOT/tools/kernel_regs.py" "$OUT/tmp/$SRC-hip-amdgcn-amd-amdhsa-gfx950.s" "$PAT" > "$OUT/regs.txt"
 rm -rf "$OUT/tmp"
 cat "$OUT/regs.txt"

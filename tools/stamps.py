@@ -39,7 +39,8 @@ for k, nm in enumerate(names):
     print(f"  {nm:12s} mean {d.mean():9.0f} p50 {np.median(d):9.0f} p90 {np.percentile(d, 90):9.0f} max {d.max():9d}")
 asp = s[:, 3] - s[:, 2]
 print(f"  in loop: iterations/wave mean {s[:, 7].mean():.2f} max {s[:, 7].max()}; scan {s[:, 5].mean():.0f} "
-      f"select {s[:, 6].mean():.0f} l2a+rest {(asp - s[:, 5] - s[:, 6]).mean():.0f} cycles/wave")
+      f"select {s[:, 6].mean():.0f} l2a+rest {(asp - s[:, 5] - s[:, 6]).mean():.0f} cycles/wave; "
+      f"first scan {s[:, 8].mean():.0f}")
 mx = it.max(axis=1)
 print("  l1 passes: lane mean", it.mean(), "wave-max mean", mx.mean(), "max", mx.max())
 for v in sorted(set(mx.tolist())):
