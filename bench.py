@@ -46,6 +46,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "motion-generation-using-quadratic-programs_amd")
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_PEAK_TFS = 78.6  # MI355X FP64 (vector and matrix) peak, AMD spec; no sparsity in FP64
 MALL_BYTES = 256 << 20  # Infinity Cache
 C4_GLOBAL = 1 << 20
 # name: (kind, n, p, m, default batch per GPU (0 = C4 split), description)
@@ -93,6 +94,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--ops-json", default=os.path.join(ROOT, "profiles", "op_counts.json"))
     return ap.parse_args(argv)
 
 
@@ -113,22 +115,38 @@ def spawn_ranks(args):
     return subprocess.call(cmd, env=dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4")))
 
 
-def cpu_baseline(pr, seconds):
+def cpu_baseline(pr, seconds, gpu_out=None):
     """The oracle (CPU restatement, -O2, 1 thread) on the same resident batch, repeated until
-    `seconds` of wall time: a bounded sample of the same workload."""
+    `seconds` of wall time: a bounded sample of the same workload.  Its first chunk is also the
+    parity sample: the GPU's x / f / status for those QPs against the oracle's (gpu_out)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
     import oracle
 
     oracle.lib()
     cap = 1000 + 100 * (pr.n + pr.p + pr.m)
-    chunk = min(pr.batch, 8192)
+    bpq = 8 * (pr.n * pr.n + pr.n + pr.n * pr.p + pr.p + pr.n * pr.m + pr.m)
+    # chunks of about the C1 chunk's work (8192 QPs of 1.8 KB): a C5 chunk is 9 QPs
+    chunk = max(1, min(pr.batch, 8192, 8192 * 1792 // bpq))
     sub = pr.slice(0, chunk)
     done = 0
+    parity = None
     t0 = time.perf_counter()
     while True:
-        oracle.solve_batch(sub, max_steps=cap, threads=1)
+        xo, fo, so, _ = oracle.solve_batch(sub, max_steps=cap, threads=1)
         done += chunk
         el = time.perf_counter() - t0
+        if parity is None and gpu_out is not None:
+            xg, fg, sg = (a[:chunk] for a in gpu_out)
+            ok = so == 0
+            def rel(a, b):
+                d = np.abs(a - b) / np.maximum(1.0, np.abs(b))
+                return float(d.max()) if d.size else 0.0
+            parity = {"qps": int(chunk), "status_equal": int((sg == so).sum()),
+                      "x_bitwise_equal": bool(np.array_equal(xg[ok].view(np.uint64), xo[ok].view(np.uint64))),
+                      "f_bitwise_equal": bool(np.array_equal(fg[ok].view(np.uint64), fo[ok].view(np.uint64))),
+                      "max_rel_err_x": rel(xg[ok], xo[ok]), "max_rel_err_f": rel(fg[ok], fo[ok]),
+                      "tolerance": 1e-10, "checker": "oracle/qp_oracle.c on the same QPs"}
         if el >= seconds:
             break
     out = {"value": done / el, "unit": "QP solves/s", "cores": 1, "kind": "port",
@@ -137,7 +155,7 @@ def cpu_baseline(pr, seconds):
     # the same restatement on the host's cores, one std::thread per core
     # over contiguous shards — capped at the CPU share a one-GPU box grants this job (16)
     threads = max(1, min(16, os.cpu_count() or 1))
-    big = pr.slice(0, min(pr.batch, 8192 * 4))
+    big = pr.slice(0, min(pr.batch, chunk * threads * 4))
     done_mt = 0
     t0 = time.perf_counter()
     while True:
@@ -156,7 +174,17 @@ def cpu_baseline(pr, seconds):
                            "sample": f"{big.batch} QPs per pass, {done_mt // big.batch} passes, "
                                      f"{el_mt:.1f} s"}
     out["cpu_model"] = model
+    if parity is not None:
+        out["parity"] = parity
     return out
+
+
+def _lib_md5():
+    import hashlib
+    try:
+        return hashlib.md5(open(os.path.join(PKG, "lib", "libqpgpu.so"), "rb").read()).hexdigest()
+    except OSError:
+        return None
 
 
 def input_set_count(args, set_bytes):
@@ -255,14 +283,15 @@ def main():
     gat = (qpdist.ResultGather(dist, rank, world, S, base.x.shape[0], n, dev, backend)
            if gather else None)
 
-    def step(k, S_=S):
+    def step(k, S_=S, use_gather=True):
         j = k % S_
         cs = streams[j]
-        if gat:
-            gat.wait(j, cs)  # slot j's record is free once its previous gather finished
+        g = gat if use_gather else None
+        if g:
+            g.wait(j, cs)  # slot j's record is free once its previous gather finished
         launcher(k % R, j, cs)()
-        if gat:
-            gat.submit(j, *outs[j], stream=cs)
+        if g:
+            g.submit(j, *outs[j], stream=cs)
 
     def sync_all():
         if gat:
@@ -272,13 +301,13 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    def timed(K, W, S_):
+    def timed(K, W, S_, use_gather=True):
         for k in range(W):
-            step(k, S_)
+            step(k, S_, use_gather)
         sync_all()
         t0 = time.perf_counter()
         for k in range(K):
-            step(W + k, S_)
+            step(W + k, S_, use_gather)
         sync_all()
         return time.perf_counter() - t0
 
@@ -295,8 +324,9 @@ def main():
     def unrot(t, r, E):
         return torch.roll(t.reshape(-1), -shifts[r] * E).reshape(t.shape)
 
+    # (TILED64: the shifts are whole 64-QP tiles, so the same flat roll un-rotates x, f, status)
     consistent = True
-    if args.layout == "qp_major":
+    if True:
         for j, r in last.items():
             x_, f_, s_ = outs[j]
             consistent &= bool(torch.equal(unrot(x_, r, n), unrot(ref_x, ref_r, n))
@@ -311,6 +341,9 @@ def main():
 
     # the same K steps on one stream (serialized launches)
     elapsed1 = timed(args.steps, 0, 1) if S > 1 else elapsed
+    # N > 1: the same K steps without the per-step gather (the solver alone), so the driver's
+    # scaling curve can separate solver scaling from rank 0's ingress
+    elapsed_solve = timed(args.steps, 0, S, use_gather=False) if gat else None
 
     # kernel-only duration for the roofline: serialized launches on one stream, HIP events on
     # that stream around each launch, rotating over the cold sets (and once more warm)
@@ -344,12 +377,33 @@ def main():
 
     gather_ms = gat.time_one() if gat else None  # one step's gather alone, same payload
 
+    # l1-pass histogram of one resident set (SURVEY.md §5 metrics): one more solve with the
+    # per-QP pass counts on
+    hb = base.__class__.__new__(base.__class__)
+    hb.__dict__.update(base.__dict__)
+    hb.x, hb.f, hb.status = (torch.empty_like(t) for t in outs[0])
+    hb.iters = torch.zeros(B, dtype=torch.int32, device=dev)
+    hb.launcher(cs, family=args.family)()
+    torch.cuda.synchronize(dev)
+    hist = torch.bincount(hb.iters[:B].to(torch.int64).clamp(min=0)).cpu().tolist()
+    gpu_sample = None
+    if world == 1 and not args.no_cpu:
+        # the QPs the CPU baseline's parity sample solves (set 0, QP order)
+        c = max(1, min(B, 8192, 8192 * 1792 // bpq))
+        xs = hb.x.reshape(-1).cpu().numpy()
+        if args.layout == "tiled64":
+            xs = qpgpu.from_tiled64(xs, B, (n,))
+        gpu_sample = (xs.reshape(-1, n)[:c], hb.f[:c].cpu().numpy(), hb.status[:c].cpu().numpy())
+
     if dist:
-        t = torch.tensor([elapsed, elapsed1, kern_cold, kern_warm, gather_ms or 0.0, kern_cold_pair],
+        t = torch.tensor([elapsed, elapsed1, kern_cold, kern_warm, gather_ms or 0.0, kern_cold_pair,
+                          elapsed_solve or 0.0],
                          dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, elapsed1, kern_cold, kern_warm = (float(v) for v in t[:4])
         kern_cold_pair = float(t[5])
+        if elapsed_solve is not None:
+            elapsed_solve = float(t[6])
         if gather:
             gather_ms = float(t[4])
         ok_t = torch.tensor([1 if consistent else 0], device=dev if backend == "nccl" else "cpu")
@@ -362,15 +416,51 @@ def main():
     total = B * world * args.steps
     achieved = bpq * B / (kern_cold * 1e-3) / 1e9
     achieved_warm = bpq * B / (kern_warm * 1e-3) / 1e9
-    traffic = traffic_src = None
+    # measured traffic: the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this config
+    # (profiles/pmc_traffic.json, calibrated read factor), with the library build they measured
+    traffic = traffic_src = traffic_build = None
     try:
         tj = json.load(open(args.traffic_json))
         key = f"{cfg}:{B}:{kname}"
         if key in tj:
             traffic = tj[key]["hbm_bytes_per_launch"]
             traffic_src = tj[key].get("source")
+            md5 = tj[key].get("libqpgpu_md5")
+            traffic_build = None if md5 is None else ("this build" if md5 == _lib_md5() else "an earlier build")
+    except (OSError, ValueError, KeyError):
+        pass
+    # algorithmic flops: the operations the reference's evaluation executes on this batch,
+    # counted by the counting build of the CPU restatement (profiles/op_counts.json,
+    # tools/op_counts.py)
+    flops_rec = None
+    try:
+        flops_rec = json.load(open(args.ops_json)).get(f"{cfg}:{B}:{args.seed}")
     except (OSError, ValueError):
         pass
+    hbm = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+           "traffic_ratio": (traffic / (bpq * B)) if traffic else None,
+           "kernel_ms": kern_cold,
+           "kernel_ms_source": f"{args.kernel_reps} serialized launches on one stream "
+                               "between one HIP-event pair (launch-to-launch average), "
+                               f"inputs rotating over {R} resident set(s)",
+           "kernel_ms_event_pair_per_launch": kern_cold_pair,
+           "warm": {"kernel_ms": kern_warm, "achieved": achieved_warm,
+                    "frac": achieved_warm / HBM_PEAK_GBS},
+           "algorithmic_bytes_per_qp": bpq,
+           "traffic_source": traffic_src, "traffic_measured_on": traffic_build}
+    compute = None
+    if flops_rec:
+        tf = flops_rec["flops"] / (kern_cold * 1e-3) / 1e12
+        compute = {"bound": "mfma", "achieved": tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                   "frac": tf / FP64_PEAK_TFS, "flops_per_launch": flops_rec["flops"],
+                   "flops_per_qp": flops_rec["per_qp"], "div_per_qp": flops_rec.get("div_per_qp"),
+                   "sqrt_per_qp": flops_rec.get("sqrt_per_qp"), "flops_source": flops_rec.get("source")}
+    # SURVEY.md §8(d) "Which roofline": HBM for C1-C4 (and the mgqp levels), FP64 compute for C5
+    primary = compute if (cfg == "C5" and compute) else hbm
+    roofline = dict(primary)
+    roofline["hbm"] = hbm
+    roofline["compute"] = compute
     par = f"batch-sharded x{world}"
     if world > 1:
         par += (f", {'RCCL' if backend == 'nccl' else backend} gather of (x, f, status) to rank 0 "
@@ -393,26 +483,21 @@ def main():
                    "streams": S, "input_sets": R, "cold_inputs": R > 1 or in_bytes * B >= 2 * MALL_BYTES,
                    "backend": backend if world > 1 else None, "parallelism": par},
         "value_streams1": total / elapsed1,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel_ms": kern_cold,
-                     "kernel_ms_source": f"{args.kernel_reps} serialized launches on one stream "
-                                         "between one HIP-event pair (launch-to-launch average), "
-                                         f"inputs rotating over {R} resident set(s)",
-                     "kernel_ms_event_pair_per_launch": kern_cold_pair,
-                     "warm": {"kernel_ms": kern_warm, "achieved": achieved_warm,
-                              "frac": achieved_warm / HBM_PEAK_GBS},
-                     "algorithmic_bytes_per_qp": bpq,
-                     "traffic_source": traffic_src},
+        "roofline": roofline,
+        "l1_pass_histogram": hist,
         "status_ok_frac": st_ok,
         "outputs_consistent": consistent,
     }
     if gather:
         out["gather_ms"] = gather_ms
         out["gather_bytes_per_rank"] = gat.bytes_per_rank
+        out["gather_bytes_per_step_into_rank0"] = gat.bytes_per_rank * (world - 1)
+        out["gather_ingress_gbs"] = gat.bytes_per_rank * (world - 1) / (gather_ms * 1e-3) / 1e9
         out["gather_verified"] = gather_ok
+        out["value_solve_only"] = total / elapsed_solve
+        out["ms_per_step_solve_only"] = elapsed_solve * 1e3 / args.steps
     if world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(pr, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(pr, args.cpu_seconds, gpu_sample)
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

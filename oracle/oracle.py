@@ -13,10 +13,11 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle_qp.so")
+COUNT_LIB_PATH = os.path.join(HERE, "liboracle_qp_count.so")  # the same code, -DQPO_COUNT
 
 
 def build(force: bool = False) -> str:
-    if force or not os.path.exists(LIB_PATH):
+    if force or not os.path.exists(LIB_PATH) or not os.path.exists(COUNT_LIB_PATH):
         subprocess.check_call(["make", "-s", "-C", HERE])
     return LIB_PATH
 
@@ -36,6 +37,46 @@ def lib():
         L.qpo_solve_batch.restype = ctypes.c_int
         _lib = L
     return _lib
+
+
+_clib = None
+
+
+def count_lib():
+    global _clib
+    if _clib is None:
+        build()
+        L = ctypes.CDLL(COUNT_LIB_PATH)
+        vp = ctypes.c_void_p
+        L.qpo_solve_batch.argtypes = [ctypes.c_int64] + [ctypes.c_int] * 3 + [vp] * 10 + [ctypes.c_int] * 3
+        L.qpo_solve_batch.restype = ctypes.c_int
+        L.qpo_op_counts.argtypes = [vp]
+        L.qpo_op_counts.restype = None
+        _clib = L
+    return _clib
+
+
+def op_counts(pr, max_steps: int = 0):
+    """Binary64 operations the reference's evaluation executes on a qpgpu.Problems batch
+    (SURVEY.md §8(d)): the counting build of the restatement solves it on one thread.
+    Returns {"mul", "add", "div", "sqrt", "flops", "per_qp"}; flops = mul + add + div + sqrt
+    (the reference has no fused multiply-add)."""
+    B, n, p, m = pr.batch, pr.n, pr.p, pr.m
+    L = count_lib()
+    out = np.zeros(4, dtype=np.uint64)
+    L.qpo_op_counts(_p(out))  # reset
+    G = np.ascontiguousarray(pr.G, dtype=np.float64)
+    arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (pr.g0, pr.CE, pr.ce0, pr.CI, pr.ci0)]
+    x = np.zeros((B, n))
+    f = np.zeros(B)
+    st = np.zeros(B, dtype=np.int32)
+    it = np.zeros(B, dtype=np.int32)
+    L.qpo_solve_batch(B, n, p, m, _p(G), *[_p(a) for a in arrs], _p(x), _p(f), _p(st), _p(it), 0,
+                      max_steps, 1)
+    L.qpo_op_counts(_p(out))
+    mul, add, div, sq = (int(v) for v in out)
+    flops = mul + add + div + sq
+    return {"mul": mul, "add": add, "div": div, "sqrt": sq, "flops": flops, "per_qp": flops / max(1, B)}
 
 
 def _p(a):

@@ -39,22 +39,48 @@
 
 #define QPO_EPS DBL_EPSILON /* std::numeric_limits<double>::epsilon(), .rodata +0x190 */
 
+/* Operation counts (SURVEY.md §8(d) "Algorithmic flops": the restatement counts the operations
+ * it actually executes, per config and seed).  Built into a separate library with -DQPO_COUNT
+ * (liboracle_qp_count.so); the timed / parity oracle has no counting code.  Counted are the
+ * binary64 operations the reference's evaluation performs: multiplications, additions and
+ * subtractions, divisions and square roots (negation, fabs, comparisons and min/max are not
+ * arithmetic and are not counted; the reference has no fused multiply-add).  Per thread. */
+#ifdef QPO_COUNT
+static __thread uint64_t qpo_cnt_mul, qpo_cnt_add, qpo_cnt_div, qpo_cnt_sqrt;
+#define CNT(mul, add, div, sq) \
+  (qpo_cnt_mul += (uint64_t)(mul), qpo_cnt_add += (uint64_t)(add), qpo_cnt_div += (uint64_t)(div), \
+   qpo_cnt_sqrt += (uint64_t)(sq))
+void qpo_op_counts(uint64_t out[4]) {
+  out[0] = qpo_cnt_mul;
+  out[1] = qpo_cnt_add;
+  out[2] = qpo_cnt_div;
+  out[3] = qpo_cnt_sqrt;
+  qpo_cnt_mul = qpo_cnt_add = qpo_cnt_div = qpo_cnt_sqrt = 0;
+}
+#else
+#define CNT(mul, add, div, sq) ((void)0)
+#endif
+
 /* distance(a, b): overflow-safe hypot, three branches (weak symbol `distance`). */
 static double qpo_distance(double a, double b) {
   double a1 = fabs(a), b1 = fabs(b), t;
   if (a1 > b1) {
+    CNT(2, 1, 1, 1);
     t = b1 / a1;
     return a1 * sqrt(1.0 + t * t);
   } else if (b1 > a1) {
+    CNT(2, 1, 1, 1);
     t = a1 / b1;
     return b1 * sqrt(1.0 + t * t);
   }
+  CNT(1, 0, 0, 0);
   return a1 * 1.4142135623730951; /* a1 * sqrt(2.0), constant at .rodata +0x1e8 */
 }
 
 /* scalar_product: left-to-right sum starting at 0.0. */
 static double qpo_dot(int n, const double *a, const double *b) {
   double s = 0.0;
+  CNT(n, n, 0, 0);
   for (int i = 0; i < n; i++) s += a[i] * b[i];
   return s;
 }
@@ -65,6 +91,7 @@ static int qpo_cholesky(int n, double *A, double *bad_sum) {
   for (int i = 0; i < n; i++) {
     for (int j = i; j < n; j++) {
       double sum = A[i * n + j];
+      CNT(i, i, i == j ? 0 : 1, i == j ? 1 : 0);
       for (int k = i - 1; k >= 0; k--) sum -= A[i * n + k] * A[j * n + k];
       if (i == j) {
         if (sum <= 0.0) {
@@ -83,6 +110,7 @@ static int qpo_cholesky(int n, double *A, double *bad_sum) {
 
 /* forward_elimination: L y = b, L lower (row-major n x n). */
 static void qpo_forward(int n, const double *L, double *y, const double *b) {
+  CNT((int64_t)n * (n - 1) / 2, (int64_t)n * (n - 1) / 2, n, 0);
   y[0] = b[0] / L[0];
   for (int i = 1; i < n; i++) {
     y[i] = b[i];
@@ -93,6 +121,7 @@ static void qpo_forward(int n, const double *L, double *y, const double *b) {
 
 /* backward_elimination: U x = y with U = the mirrored upper triangle. */
 static void qpo_backward(int n, const double *U, double *x, const double *y) {
+  CNT((int64_t)n * (n - 1) / 2, (int64_t)n * (n - 1) / 2, n, 0);
   x[n - 1] = y[n - 1] / U[(n - 1) * n + (n - 1)];
   for (int i = n - 2; i >= 0; i--) {
     x[i] = y[i];
@@ -103,6 +132,7 @@ static void qpo_backward(int n, const double *U, double *x, const double *y) {
 
 /* compute_d: d = J^T np, column dots with j ascending. */
 static void qpo_compute_d(int n, double *d, const double *J, const double *np) {
+  CNT((int64_t)n * n, (int64_t)n * n, 0, 0);
   for (int i = 0; i < n; i++) {
     double sum = 0.0;
     for (int j = 0; j < n; j++) sum += J[j * n + i] * np[j];
@@ -112,6 +142,7 @@ static void qpo_compute_d(int n, double *d, const double *J, const double *np) {
 
 /* update_z: z = J[:, iq:] d[iq:]. */
 static void qpo_update_z(int n, double *z, const double *J, const double *d, int iq) {
+  CNT((int64_t)n * (n - iq), (int64_t)n * (n - iq), 0, 0);
   for (int i = 0; i < n; i++) {
     z[i] = 0.0;
     for (int j = iq; j < n; j++) z[i] += J[i * n + j] * d[j];
@@ -122,6 +153,7 @@ static void qpo_update_z(int n, double *z, const double *J, const double *d, int
 static void qpo_update_r(int n, const double *R, double *r, const double *d, int iq) {
   for (int i = iq - 1; i >= 0; i--) {
     double sum = 0.0;
+    CNT(iq - 1 - i, iq - i, 1, 0);
     for (int j = i + 1; j < iq; j++) sum += R[i * n + j] * r[j];
     r[i] = (d[i] - sum) / R[i * n + i];
   }
@@ -135,6 +167,7 @@ static int qpo_add_constraint(int n, double *R, double *J, double *d, int *iq, d
     double cc = d[j - 1], ss = d[j];
     double h = qpo_distance(cc, ss);
     if (fabs(h) < QPO_EPS) continue;
+    CNT(3 * n, 1 + 3 * n, 3, 0);
     d[j] = 0.0;
     ss = ss / h;
     cc = cc / h;
@@ -187,6 +220,7 @@ static void qpo_delete_constraint(int n, double *R, double *J, int *A, double *u
     double cc = R[j * n + j], ss = R[(j + 1) * n + j];
     double h = qpo_distance(cc, ss);
     if (fabs(h) < QPO_EPS) continue;
+    CNT(3 * (*iq - j - 1) + 3 * n, 1 + 3 * (*iq - j - 1) + 3 * n, 3, 0);
     cc = cc / h;
     ss = ss / h;
     R[(j + 1) * n + j] = 0.0;
@@ -243,6 +277,7 @@ int qpo_solve(int n, int p, int m, double *G, const double *g0, const double *CE
 
   /* c1 = trace(G) before factorisation */
   c1 = 0.0;
+  CNT(0, n, 0, 0);
   for (int i = 0; i < n; i++) c1 += G[i * n + i];
   {
     double bad;
@@ -260,6 +295,7 @@ int qpo_solve(int n, int p, int m, double *G, const double *g0, const double *CE
     d[i] = 1.0;
     qpo_forward(n, G, z, d);
     for (int j = 0; j < n; j++) J[i * n + j] = z[j];
+    CNT(0, 1, 0, 0);
     c2 += z[i];
     d[i] = 0.0;
   }
@@ -267,6 +303,7 @@ int qpo_solve(int n, int p, int m, double *G, const double *g0, const double *CE
   qpo_forward(n, G, tmp, g0);
   qpo_backward(n, G, x, tmp);
   for (int i = 0; i < n; i++) x[i] = -x[i];
+  CNT(1, 0, 0, 0);
   f_value = 0.5 * qpo_dot(n, g0, x);
 
   /* equality constraints */
@@ -277,7 +314,11 @@ int qpo_solve(int n, int p, int m, double *G, const double *g0, const double *CE
     qpo_update_z(n, z, J, d, iq);
     qpo_update_r(n, R, r, d, iq);
     t2 = 0.0;
-    if (fabs(qpo_dot(n, z, z)) > QPO_EPS) t2 = (-qpo_dot(n, np, x) - ce0[i]) / qpo_dot(n, z, np);
+    if (fabs(qpo_dot(n, z, z)) > QPO_EPS) {
+      CNT(0, 1, 1, 0);
+      t2 = (-qpo_dot(n, np, x) - ce0[i]) / qpo_dot(n, z, np);
+    }
+    CNT(n + iq + 3, n + iq + 1, 0, 0);
     for (int k = 0; k < n; k++) x[k] += t2 * z[k];
     u[iq] = t2;
     for (int k = 0; k < iq; k++) u[k] -= t2 * r[k];
@@ -301,6 +342,7 @@ l1:
   ss = 0.0;
   psi = 0.0;
   ip = 0;
+  CNT((int64_t)m * n + 4, (int64_t)m * (n + 2), 0, 0);
   for (int i = 0; i < m; i++) {
     iaexcl[i] = 1;
     sum = 0.0;
@@ -347,13 +389,16 @@ l2a:
   t1 = inf;
   for (int k = p; k < iq; k++) {
     if (r[k] > 0.0) {
+      CNT(0, 0, 1, 0);
       if (u[k] / r[k] < t1) {
+        CNT(0, 0, 1, 0);
         t1 = u[k] / r[k];
         l = A[k];
       }
     }
   }
   if (fabs(qpo_dot(n, z, z)) > QPO_EPS) {
+    CNT(0, 0, 1, 0);
     t2 = -s[ip] / qpo_dot(n, z, np);
     if (t2 < 0) t2 = inf; /* Takano Akio patch */
   } else {
@@ -367,6 +412,7 @@ l2a:
   }
   if (t2 >= inf) {
     /* dual step only */
+    CNT(iq, iq + 1, 0, 0);
     for (int k = 0; k < iq; k++) u[k] -= t * r[k];
     u[iq] += t;
     iai[l] = l;
@@ -374,6 +420,7 @@ l2a:
     goto l2a;
   }
   /* primal and dual step */
+  CNT(n + 3 + iq, n + 2 + iq + 2, 0, 0);
   for (int k = 0; k < n; k++) x[k] += t * z[k];
   f_value += t * qpo_dot(n, z, np) * (0.5 * t + u[iq]);
   for (int k = 0; k < iq; k++) u[k] -= t * r[k];
@@ -400,6 +447,7 @@ l2a:
   iai[l] = l;
   qpo_delete_constraint(n, R, J, A, u, p, &iq, l);
   sum = 0.0;
+  CNT(n, n + 1, 0, 0);
   for (int k = 0; k < n; k++) sum += CI[k * m + ip] * x[k];
   s[ip] = sum + ci0[ip];
   goto l2a;

@@ -28,6 +28,11 @@ for s in $STEPS; do
     pytest) run pytest 900 python -m pytest tests -m gpu -q -rf ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
+    benchfull)
+      # every config's line with its CPU baseline (bounded sample) and parity sample
+      for c in ${CFGS:-C1 C2 mgqp C3}; do run benchfull_$c 900 python bench.py --config $c --steps 20 --cpu-seconds 10; done
+      case " ${CFGS:-C1 C2 mgqp C3 C5} " in *" C5 "*) run benchfull_C5 900 python bench.py --config C5 --steps 3 --warmup 1 --kernel-reps 3 --cpu-seconds 10 ;; esac ;;
+    benchtiled) run bench_tiled64 600 python bench.py --layout tiled64 --no-cpu --steps 20 ;;
     benchfam)
       for f in ${FAMILIES:-lane subgroup}; do for l in qp_major tiled64; do run bench_${f}_$l 600 python bench.py --family $f --layout $l --no-cpu; done; done ;;
     benchall)
@@ -51,7 +56,6 @@ for s in $STEPS; do
     trace3) run trace3 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace3" -o c1 -- python3 bench.py --steps 20 --warmup 5 --no-cpu ;;
     profC3) run profC3 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profC3" -o c3 -- python3 bench.py --config C3 --steps 5 --warmup 1 --no-cpu --streams 1 --kernel-reps 3 ;;
     profC5) run profC5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profC5" -o c5 -- python3 bench.py --config C5 --steps 3 --warmup 1 --no-cpu --streams 1 --kernel-reps 2 ;;
-    profC5) run profC5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profC5" -o c5 -- python3 bench.py --config C5 --steps 2 --warmup 1 --no-cpu --streams 1 --kernel-reps 2 ;;
     pmcC5)
       run pmcC5_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcC5_fetch" -o c5 -- python3 bench.py --config C5 --steps 2 --warmup 1 --no-cpu --streams 1 --kernel-reps 1
       run pmcC5_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcC5_write" -o c5 -- python3 bench.py --config C5 --steps 2 --warmup 1 --no-cpu --streams 1 --kernel-reps 1
@@ -108,6 +112,20 @@ import csv, statistics, sys
 vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(sys.argv[1] + "c1_counter_collection.csv")) if "qp_lane" in r["Kernel_Name"]]
 print(sys.argv[1], "FETCH_SIZE KiB median", statistics.median(vals), "-> bytes x2", 2 * 1024 * statistics.median(vals))
 PY
+      done ;;
+    calib)
+      # FETCH_SIZE / WRITE_SIZE calibration for the solver's access patterns (tools/fetch_probe.hip)
+      run calib_fetch 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_fetch" -o probe -- ./tools/fetch_probe
+      run calib_write 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/calib_write" -o probe -- ./tools/fetch_probe
+      python3 tools/pmc_calib.py "$OUT/calib_fetch" "$OUT/calib_write" "$OUT/pmc_calibration.json" ;;
+    pmccfg)
+      # FETCH_SIZE and WRITE_SIZE passes of one config's bench (CFG), one pass per counter
+      for c in ${CFGS:-C1}; do
+        case $c in C5) xa="--steps 2 --warmup 1 --kernel-reps 1";; C3) xa="--steps 3 --warmup 1 --kernel-reps 2";; *) xa="--steps 5 --warmup 1 --kernel-reps 3";; esac
+        run pmc_fetch_$c 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$c" -o k -- python3 bench.py --config $c --no-cpu --streams 1 $xa
+        run pmc_write_$c 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$c" -o k -- python3 bench.py --config $c --no-cpu --streams 1 $xa
+        read B K < <(python3 -c "import sys; sys.path.insert(0, 'motion-generation-using-quadratic-programs_amd'); import bench, qpgpu; c = bench.CONFIGS['$c']; print(c[4], qpgpu.kernel_name(c[1], c[2], c[3]))")
+        python3 tools/pmc_traffic.py "$OUT/pmc_fetch_$c" "$OUT/pmc_write_$c" $c $B "$K" "$OUT/pmc_traffic.json"
       done ;;
     listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;
     sq)
