@@ -90,10 +90,13 @@ enum qpgpu_error {
                                           everywhere, so x and f are bit-identical to the CPU
                                           restatement of QuadProg++'s order (SURVEY §3.2;
                                           reference-pinned on the demo KAT only).
-                                          Shapes up to n = 64 always do; for n > 64 the default
-                                          runs the O(n^3) setup (Cholesky, J = L^-T, x0) as
-                                          blocked f64 MFMA (qp_panel.hip), which matches the
-                                          reference within 1e-10 relative instead.  Implied by
+                                          Shapes with n <= 64 and m <= 256 always do.  The
+                                          others (n > 64, or m > 256, which the workspace
+                                          variant serves) by default run the O(n^3) setup
+                                          (Cholesky, J = L^-T, x0) as blocked f64 MFMA
+                                          (qp_panel.hip) and the loop's d, z, r sums as tree
+                                          sums, which match within 1e-10 relative (same status
+                                          and iteration counts) instead.  Implied by
                                           QPGPU_FLAG_WRITE_FACTOR. */
 
 /* Kernel-family selection (benchmarking / testing knobs; default = fastest for the shape):

@@ -782,7 +782,13 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   uint64_t tph[6] = {0, 0, 0, 0, 0, 0}, teq[5] = {0, 0, 0, 0, 0}, tdet[3] = {0, 0, 0};
   auto clk = [&]() -> uint64_t { return (QPGPU_WAVE_STAMPS && a.stamps) ? __builtin_amdgcn_s_memtime() : 0; };
   // iq0 of an add_constraint whose J sweep was deferred into the next d/z pass, or -1
-  // (tolerance mode, QPGPU_WAVE_TOLLOOP bit 2; the same value in every lane)
+  // (tolerance mode, QPGPU_WAVE_TOLLOOP bit 2; the same value in every lane).  A QP can finish
+  // with a sweep still pending (no violated constraint after a successful add, or the step
+  // cap): its J in the workspace is then not the reference's final J.  Nothing reads J after
+  // the loop in this mode — J reaches the caller only through QPGPU_FLAG_WRITE_FACTOR (G, the
+  // factor, not J) and EXACT runs, and uses_panel() sends both of those to the serial path
+  // (defer needs `pre`, which only the panel setup sets).  A future J export from this path
+  // must first apply the pending sweep (plain_sweep with iq0 = pend).
   int pend = -1;
   constexpr bool kDefer = GJR && (QPGPU_WAVE_TOLLOOP & 4) && (QPGPU_WAVE_TOLLOOP & 1) && S == 4 * 64 && NMAX <= S;
   auto compute_d_z = [&](int iq) {
@@ -1991,6 +1997,8 @@ extern "C" hipError_t qpk_launch_panel_setup(const qpk::QpArgs* a, hipStream_t s
 // Workspace variants (n > 64) run the MFMA panel setup (qp_panel.hip) first unless the caller
 // asked for the reference's exact operation order (QPGPU_FLAG_EXACT) or for the factor in G
 // (QPGPU_FLAG_WRITE_FACTOR: the reference's bits), which the serial restatement here provides.
+// Only panel-set-up launches run the tolerance-mode loop, whose deferred J sweep may still be
+// pending when a QP finishes (see `pend` in qp_wave_kernel): keep both flags out of it.
 static bool uses_panel(const qpk::WaveVariant* v, uint32_t flags) {
   return v->ws_doubles_per_qp > 0 && !(flags & (QPGPU_FLAG_EXACT | QPGPU_FLAG_WRITE_FACTOR));
 }

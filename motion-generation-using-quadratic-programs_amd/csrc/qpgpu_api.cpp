@@ -247,7 +247,8 @@ static bool family_covers(uint32_t flags, int n, int p, int m) {
 // copy of [x | f | status | iters] (+ G with WRITE_FACTOR) — instead of 7 + 4 pageable copies —
 // which is what a 50 ms control cycle's single solves need (latency, tools/dropin_latency.cpp).
 // Larger batches copy each array directly (a host-side pack would only add a pass over them).
-// QPGPU_HOST_STAGING=0 forces the direct copies (A/B measurement).
+// Measured for one C1 QP (profiles/r02_s3/latency.log): 41 us p50 staged, 114 us with per-array
+// copies.
 static constexpr size_t kStagedBytes = 4u << 20;
 
 struct PinnedStage {
@@ -258,15 +259,6 @@ struct PinnedStage {
   }
 };
 thread_local PinnedStage g_pin;
-
-static bool staging_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("QPGPU_HOST_STAGING");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
 
 int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const double* g0,
                              const double* CE, const double* ce0, const double* CI,
@@ -318,7 +310,7 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const doubl
   double* dG = D(oG);
   hipStream_t s = g_ws.stream;
   const bool wf = (d->flags & QPGPU_FLAG_WRITE_FACTOR) != 0;
-  const bool staged = staging_enabled() && total <= kStagedBytes;
+  const bool staged = total <= kStagedBytes;
   // after a failure past the first queued copy, drain the stream before returning so no copy
   // still reads or writes the caller's buffers
   auto fail_drain = [&](hipError_t err, const char* what) {

@@ -7,7 +7,7 @@ float glue around them (Eigen products and JacobiSVD in the reference) is parity
 outputs are compared with float tolerances: 1e-4 x max(1, |output|) (measured: <= 3e-7).  Robots
 whose hierarchy hits a numerically dependent level (a solve with |f| > 1e8, where the dual step
 blows up and the answer depends on the last float bits — chaotic in the reference too) are
-excluded and counted; they must stay rare.  The batched path must equal the single-cycle path
+excluded, listed and counted; they must stay at the measured rate (<= 1 in 400).  The batched path must equal the single-cycle path
 bit for bit (same host arithmetic, bitwise solver).
 
 Every check takes the controller library as a parameter: test_mgqp_host.py runs the same checks
@@ -41,30 +41,38 @@ def _close(a, b):
     np.testing.assert_allclose(a, b, rtol=0, atol=1e-4 * scale)
 
 
+def _check_ill(ill, checked):
+    """Robots excluded as ill-conditioned (|f| > 1e8 in some level) must stay at the measured
+    rate, <= 1 in 400; the failure lists them."""
+    assert len(ill) <= checked // 400, f"{len(ill)} of {checked} robots excluded as ill-conditioned: {ill}"
+
+
 def _ctl(lib=None):
     return mgqp.ops_controller(library=lib)
 
 
 @pytest.mark.parametrize("wide", [False, True])
 def test_update_hook_matches_oracle(gpu, wide, lib=LIB):
-    sc = mgqp.make_scenario(48, seed=5)
+    # 400 robots, so the <= 1-in-400 allowance is one robot (measured: 0 of 1200 robots in the
+    # ops configuration, 1 of 1200 — robot 9 of this scenario — in the wide one)
+    sc = mgqp.make_scenario(400, seed=5)
     c, o = _ctl(lib), mo.ops_oracle()
     if wide:
         _wide(c, o)
-    ill = 0
+    ill = []
     for r in range(sc.count):
         code, tq, tr, lim = c.updateHook(sc.robot(r))
         ocode, otq, otr = o.update(sc, r)
         assert code == ocode == 0
         if o.ill_conditioned:
-            ill += 1
+            ill.append(r)
             continue
         _close(tr, otr)
         _close(tq, otq)
         # out_jointAccDynLimitSup keeps the reference defect (src/mgqp.cpp:1161)
         np.testing.assert_array_equal(lim["jointAccDynLimitSup"], np.full(7, 5, np.float32))
         np.testing.assert_array_equal(lim["jointTorqueLimitInf"], np.full(7, -100, np.float32))
-    assert ill <= sc.count // 20
+    _check_ill(ill, sc.count)
 
 
 def test_batched_equals_single_bitwise(gpu, lib=LIB):
@@ -88,15 +96,15 @@ def test_batched_wide_mixed_feasibility(gpu, lib=LIB):
     _wide(c, o)
     codes, tq, tr = c.update_batched(sc)
     assert (codes == 0).all()
-    ill = 0
+    ill = []
     for r in range(0, sc.count, 4):
         _, otq, otr = o.update(sc, r)
         if o.ill_conditioned:
-            ill += 1
+            ill.append(r)
             continue
         _close(tr[r], otr)
         _close(tq[r], otq)
-    assert ill <= 4
+    _check_ill(ill, len(range(0, sc.count, 4)))
 
 
 def test_joint_beyond_limit_nan_log(gpu, lib=LIB):

@@ -5,7 +5,6 @@
 // inequalities), against the 50 ms control period of ops/mgqp.ops:184.
 //
 // usage: dropin_latency [solves] [cycles]      (prints one JSON line)
-// QPGPU_HOST_STAGING=0 selects the per-array copies of qpgpu_solve_batched_host (A/B).
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -135,13 +134,12 @@ int main(int argc, char** argv) {
     }
   }
   const Stats a = stats(t_solve), b = stats(t_cycle);
-  const char* st = std::getenv("QPGPU_HOST_STAGING");
   std::printf(
       "{\"what\": \"BASELINE config 1: one solve_quadprog() / one updateHook cycle, host to host\", "
       "\"staging\": \"%s\", \"solve_us\": {\"p50\": %.2f, \"p99\": %.2f, \"mean\": %.2f, \"max\": %.2f, "
       "\"n\": %d, \"finite\": %d}, \"cycle_us\": {\"p50\": %.2f, \"p99\": %.2f, \"mean\": %.2f, "
       "\"max\": %.2f, \"n\": %d, \"written\": %d}, \"period_us\": 50000}\n",
-      (st && st[0] == '0') ? "per-array copies" : "pinned, 1 H2D + 1 D2H", a.p50, a.p99, a.mean,
+      "pinned, 1 H2D + 1 D2H", a.p50, a.p99, a.mean,
       a.max, solves, ok, b.p50, b.p99, b.mean, b.max, cycles, written);
   return 0;
 }

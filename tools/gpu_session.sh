@@ -46,11 +46,7 @@ for s in $STEPS; do
       run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --streams 1
       run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --streams 1
       python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" C1 65536 "$(python3 -c 'import sys; sys.path.insert(0,"motion-generation-using-quadratic-programs_amd"); import qpgpu; print(qpgpu.kernel_name(7,6,14))')" "$OUT/pmc_traffic.json" ;;
-    benchj)
-      for j in 0 1; do for l in qp_major tiled64; do QPGPU_LANE_JREG=$j run bench_jreg${j}_$l 600 python bench.py --family lane --layout $l --no-cpu; done; done ;;
     stamps) for l in qp_major tiled64; do run stamps_general_$l 300 python tools/stamps.py general $l; run stamps_box_$l 300 python tools/stamps.py box $l; done ;;
-    benchqpw)
-      for q in 64 32; do QPGPU_LANE_QPW=$q run bench_qpw$q 600 python bench.py --family lane --no-cpu; done ;;
     dist2) run dist2 600 python bench.py --gpus 2 --steps 10 --warmup 2 ;;
     dist2c1) run dist2c1 600 python bench.py --gpus 2 --config C1 --steps 10 --warmup 2 ;;
     trace3) run trace3 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace3" -o c1 -- python3 bench.py --steps 20 --warmup 5 --no-cpu ;;
@@ -64,8 +60,7 @@ for s in $STEPS; do
       for c in C1 C2 mgqp C3; do run benchcold_$c 600 python bench.py --config $c --no-cpu --steps 20; done
       run benchcold_C5 600 python bench.py --config C5 --no-cpu --steps 3 --warmup 1 --kernel-reps 3 ;;
     latency)
-      run latency 300 tools/dropin_latency 2000 500
-      QPGPU_HOST_STAGING=0 run latency_nostage 300 tools/dropin_latency 2000 500 ;;
+      run latency 300 tools/dropin_latency 2000 500 ;;
     ab)
       # A/B of the in-tree build against _ab/<variant>/libqpgpu.so (tools/ab_build.sh), per config
       for c in ${CONFIGS:-C1 C2}; do
@@ -100,9 +95,6 @@ for s in $STEPS; do
       run sqB_$c 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d "$OUT/sqB_$c" -o c1 -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu --streams 1 --kernel-reps 1
       run sqC_$c 600 rocprofv3 --pmc SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH --output-format csv -d "$OUT/sqC_$c" -o c1 -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu --streams 1 --kernel-reps 1
       python3 tools/sqsum.py "$OUT" > "$OUT/sqsum_$c.log" 2>&1; cat "$OUT/sqsum_$c.log" ;;
-    c5res)
-      # C5 with the number of resident QPs per CU capped (Infinity-Cache residency experiment)
-      for k in ${CAPS:-1 2 4}; do QPGPU_WAVE_GJR_BLOCKS_PER_CU=$k run bench_C5_cap$k 600 python bench.py --config C5 --no-cpu --steps 2 --warmup 1 --kernel-reps 2; done ;;
     abpmc)
       # FETCH_SIZE of the C1 kernel for the in-tree build and each A/B variant (one pass each)
       run pmcab_base 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcab_base" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --streams 1
@@ -130,7 +122,6 @@ PY
     listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;
     sq)
       for f in ${FAMILIES:-lane subgroup}; do
-        export QPGPU_LANE_JREG=${JREG:-0}
         run sqA_$f 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d "$OUT/sqA_$f" -o c1 -- python3 bench.py --steps 3 --warmup 1 --no-cpu --family $f --layout ${LAYOUT:-qp_major}
         run sqB_$f 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d "$OUT/sqB_$f" -o c1 -- python3 bench.py --steps 3 --warmup 1 --no-cpu --family $f --layout ${LAYOUT:-qp_major}
         run sqC_$f 600 rocprofv3 --pmc SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH --output-format csv -d "$OUT/sqC_$f" -o c1 -- python3 bench.py --steps 3 --warmup 1 --no-cpu --family $f --layout ${LAYOUT:-qp_major}
