@@ -32,6 +32,12 @@ for s in $STEPS; do
       # every config's line with its CPU baseline (bounded sample) and parity sample
       for c in ${CFGS:-C1 C2 mgqp C3}; do run benchfull_$c 900 python bench.py --config $c --steps 20 --cpu-seconds 10; done
       case " ${CFGS:-C1 C2 mgqp C3 C5} " in *" C5 "*) run benchfull_C5 900 python bench.py --config C5 --steps 3 --warmup 1 --kernel-reps 3 --cpu-seconds 10 ;; esac ;;
+    c5res)
+      # C5 with fewer resident QPs (Infinity-Cache residency experiment): one warm input set,
+      # batch B (160 QPs x 1.5 MiB of CI + J ~ 240 MiB fits the 256 MiB Infinity Cache)
+      for b in ${C5B:-160 256 512 4096}; do run bench_C5_b$b 600 python bench.py --config C5 --batch $b --input-sets 1 --no-cpu --steps 3 --warmup 1 --kernel-reps 2 --streams 1; done ;;
+    fastdiag)
+      for v in ${VARIANTS}; do QPGPU_LIB_PATH=_ab/$v/libqpgpu.so run fastdiag_$v 600 python tools/fast_diag.py C1 C2; done ;;
     benchtiled) run bench_tiled64 600 python bench.py --layout tiled64 --no-cpu --steps 20 ;;
     benchfam)
       for f in ${FAMILIES:-lane subgroup}; do for l in qp_major tiled64; do run bench_${f}_$l 600 python bench.py --family $f --layout $l --no-cpu; done; done ;;
