@@ -9,7 +9,7 @@ shift 2
 for attempt in 1 2 3 4 5 6 7 8; do
   timeout $((TO + 900)) /usr/local/graft/bin/gpurun --timeout "$TO" -- "$@" > "$LOG" 2>&1
   rc=$?
-  if grep -q "stopped responding while being prepared\|slot(s) on this pod are busy\|backing off\|no box\|no free box" "$LOG" &&
+  if grep -q "stopped responding while being prepared\|slot(s) on this pod are busy\|backing off\|no box\|no free box\|taken away by the GPU service" "$LOG" &&
      ! grep -q "status=ok" "$LOG"; then
     echo "attempt $attempt: no box ($(grep -o 'status=[a-z]*' "$LOG" | head -1)); waiting" >&2
     sleep 90
