@@ -115,6 +115,12 @@ def spawn_ranks(args):
     return subprocess.call(cmd, env=dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4")))
 
 
+def cpu_chunk(pr):
+    """QPs per CPU-baseline chunk: about the C1 chunk's work (8192 QPs of 1.8 KB); C5: 9 QPs."""
+    bpq = 8 * (pr.n * pr.n + pr.n + pr.n * pr.p + pr.p + pr.n * pr.m + pr.m) + 8 * (pr.n + 1)
+    return max(1, min(pr.batch, 8192, 8192 * 1792 // bpq))
+
+
 def cpu_baseline(pr, seconds, gpu_out=None):
     """The oracle (CPU restatement, -O2, 1 thread) on the same resident batch, repeated until
     `seconds` of wall time: a bounded sample of the same workload.  Its first chunk is also the
@@ -125,9 +131,7 @@ def cpu_baseline(pr, seconds, gpu_out=None):
 
     oracle.lib()
     cap = 1000 + 100 * (pr.n + pr.p + pr.m)
-    bpq = 8 * (pr.n * pr.n + pr.n + pr.n * pr.p + pr.p + pr.n * pr.m + pr.m)
-    # chunks of about the C1 chunk's work (8192 QPs of 1.8 KB): a C5 chunk is 9 QPs
-    chunk = max(1, min(pr.batch, 8192, 8192 * 1792 // bpq))
+    chunk = cpu_chunk(pr)
     sub = pr.slice(0, chunk)
     done = 0
     parity = None
@@ -389,7 +393,7 @@ def main():
     gpu_sample = None
     if world == 1 and not args.no_cpu:
         # the QPs the CPU baseline's parity sample solves (set 0, QP order)
-        c = max(1, min(B, 8192, 8192 * 1792 // bpq))
+        c = cpu_chunk(pr)
         xs = hb.x.reshape(-1).cpu().numpy()
         if args.layout == "tiled64":
             xs = qpgpu.from_tiled64(xs, B, (n,))

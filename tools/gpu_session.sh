@@ -38,6 +38,12 @@ for s in $STEPS; do
       for b in ${C5B:-160 256 512 4096}; do run bench_C5_b$b 600 python bench.py --config C5 --batch $b --input-sets 1 --no-cpu --steps 3 --warmup 1 --kernel-reps 2 --streams 1; done ;;
     fastdiag)
       for v in ${VARIANTS}; do QPGPU_LIB_PATH=_ab/$v/libqpgpu.so run fastdiag_$v 600 python tools/fast_diag.py C1 C2; done ;;
+    profcfg)
+      # rocprofv3 kernel trace + stats of one config's bench (serialized launches), per config
+      for c in ${CFGS:-C1}; do
+        case $c in C5) xa="--steps 3 --warmup 1 --kernel-reps 2";; C3) xa="--steps 5 --warmup 1 --kernel-reps 3";; *) xa="--steps 20 --warmup 5";; esac
+        run prof_$c 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$c" -o k -- python3 bench.py --config $c --no-cpu --streams 1 $xa
+      done ;;
     benchtiled) run bench_tiled64 600 python bench.py --layout tiled64 --no-cpu --steps 20 ;;
     benchfam)
       for f in ${FAMILIES:-lane subgroup}; do for l in qp_major tiled64; do run bench_${f}_$l 600 python bench.py --family $f --layout $l --no-cpu; done; done ;;
