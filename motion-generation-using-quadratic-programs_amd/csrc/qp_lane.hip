@@ -239,14 +239,22 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
     stage_all(a.G, n * n, 0);
     stage_all(a.g0, n, offg0);
     __syncthreads();
+    // The LDS reads are unconditional (in range for every lane; an idle lane's slot holds stale
+    // data that the select drops): a read under `live` becomes one exec-masked block per element,
+    // which the scheduler can neither pair nor overlap.
     double g0v[NM];
 #pragma unroll
     for (int i = 0; i < NM; i++) {
 #pragma unroll
-      for (int j = 0; j < NM; j++) Gr[i][j] = (live && i < n && j < n) ? rd_all(0, n * n, i * n + j) : 0.0;
-      g0v[i] = (live && i < n) ? rd_all(offg0, n, i) : 0.0;
+      for (int j = 0; j < NM; j++) {
+        const double v = (i < n && j < n) ? rd_all(0, n * n, i * n + j) : 0.0;
+        Gr[i][j] = live ? v : 0.0;
+      }
+      const double v0 = i < n ? rd_all(offg0, n, i) : 0.0;
+      g0v[i] = live ? v0 : 0.0;
     }
     __syncthreads();
+    qp_stamp(a, 9);  // diagnostic: G / g0 in registers
     // round B: CE and ce0 (equality phase), issued now so they land during the Cholesky
     if (p > 0) {
       const int np_ = n * p;
@@ -299,15 +307,23 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
       const int offc = (kQpw * np_ + 127) / 128 * 128;
       ce_staged = offc + kQpw * p <= STAGE;
       __syncthreads();
+      qp_stamp(a, 10);  // diagnostic: round B (CE) landed
       if constexpr (kCiDma && PX > 0) {
         if (dma && ce_staged) {
           // CE / ce0 -> AGPRs, then the LDS is the CI copy's (round C)
 #pragma unroll
-          for (int e = 0; e < NM * PX; e++) ceag[e] = to_agpr(live ? rd_all(0, np_, e) : 0.0);
+          for (int e = 0; e < NM * PX; e++) {
+            const double v = rd_all(0, np_, e);
+            ceag[e] = to_agpr(live ? v : 0.0);
+          }
 #pragma unroll
-          for (int e = 0; e < PX; e++) ceag[NM * PX + e] = to_agpr(live ? rd_all(offc, p, e) : 0.0);
+          for (int e = 0; e < PX; e++) {
+            const double v = rd_all(offc, p, e);
+            ceag[NM * PX + e] = to_agpr(live ? v : 0.0);
+          }
           ce_agpr = true;
           __syncthreads();
+          qp_stamp(a, 11);  // diagnostic: CE in AGPRs
           // the rows past the LDS copy (and ci0) warmed here; the copy itself goes a part per
           // equality step.  Measured (profiles/r03_s10): C1 kernel 47.4 us with the warm-up
           // here, 48.6 without it, 49.9 with it at the first equality step
@@ -615,23 +631,32 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
         for (int j = 0; j < NM; j++) {
           if constexpr (kCiDma && PX > 0) {
             if (ce_agpr) {
-              npv[j] = (live && j < n) ? from_agpr(ceag[(j * PX + i) < kCeN ? j * PX + i : 0]) : 0.0;
+              // (idle lanes' ceag already holds zeros)
+              npv[j] = j < n ? from_agpr(ceag[(j * PX + i) < kCeN ? j * PX + i : 0]) : 0.0;
               continue;
             }
           }
-          npv[j] = (live && j < n) ? (ce_staged ? rd_all(0, np_, j * p + i)
-                                                : view(const_cast<double*>(a.CE), np_)[(j * p + i) * T])
-                                   : 0.0;
+          if (ce_staged) {  // unconditional LDS read, then the select (see the G reads)
+            const double v = j < n ? rd_all(0, np_, j * p + i) : 0.0;
+            npv[j] = live ? v : 0.0;
+          } else {
+            npv[j] = (live && j < n) ? view(const_cast<double*>(a.CE), np_)[(j * p + i) * T] : 0.0;
+          }
         }
         bool c0_done = false;
         if constexpr (kCiDma && PX > 0) {
           if (ce_agpr) {
-            c0 = live ? from_agpr(ceag[NM * PX + i < kCeN ? NM * PX + i : 0]) : 0.0;
+            c0 = from_agpr(ceag[NM * PX + i < kCeN ? NM * PX + i : 0]);
             c0_done = true;
           }
         }
         if (!c0_done)
-          c0 = live ? (ce_staged ? rd_all(offc, p, i) : view(const_cast<double*>(a.ce0), p)[i * T]) : 0.0;
+          if (ce_staged) {
+            const double v = rd_all(offc, p, i);
+            c0 = live ? v : 0.0;
+          } else {
+            c0 = live ? view(const_cast<double*>(a.ce0), p)[i * T] : 0.0;
+          }
       } else {  // p > n: the step that reports "dependent" (reference UB, see oracle)
         const double* CEb = view(const_cast<double*>(a.CE), n * p);
 #pragma unroll

@@ -46,5 +46,15 @@ print("  l1 passes: lane mean", it.mean(), "wave-max mean", mx.mean(), "max", mx
 for v in sorted(set(mx.tolist())):
     sel = mx == v
     print(f"    wave-max {v}: {sel.sum():5d} waves, active-set cycles mean {(s[sel, 3] - s[sel, 2]).mean():.0f}")
+if (s[:, 9] > 0).all():
+    g = s[:, 9] - s[:, 0]
+    print(f"  setup detail: G landed+read {g.mean():.0f}", end="")
+    if (s[:, 10] > 0).all():
+        print(f", Cholesky + round-B wait {(s[:, 10] - s[:, 9]).mean():.0f}", end="")
+        if (s[:, 11] > 0).all():
+            print(f", CE -> AGPR {(s[:, 11] - s[:, 10]).mean():.0f}, J + solve {(s[:, 1] - s[:, 11]).mean():.0f}", end="")
+        else:
+            print(f", J + solve {(s[:, 1] - s[:, 10]).mean():.0f}", end="")
+    print()
 start = s[:, 0] - s[:, 0].min()
 print("  wave start offsets (cycles): p50", np.median(start), "max", start.max(), " end max", (s[:, 4] - s[:, 0].min()).max())
