@@ -133,14 +133,14 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
   // range into sbuf with LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave-instruction, no
   // VGPRs, everything in flight at once); a partial last QP-major wave copies per lane.
   const bool full = (T == 64) || (valid == kQpw);
+  auto copy_chunk = [&](const double* src, int nd, int off, int k) {  // doubles [k, k+128)
+    const int e = k + 2 * lane;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(e < nd ? src + e : src),
+                                     (__attribute__((address_space(3))) void*)(sbuf + off + k), 16, 0, 0);
+  };
   auto copy_span = [&](const double* src, int nd, int off) {  // nd even, full waves only
 #pragma unroll 4
-    for (int k = 0; k < nd; k += 128) {
-      const int e = k + 2 * lane;
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(e < nd ? src + e : src),
-          (__attribute__((address_space(3))) void*)(sbuf + off + k), 16, 0, 0);
-    }
+    for (int k = 0; k < nd; k += 128) copy_chunk(src, nd, off, k);
   };
   // whole tile of X (E doubles per QP) -> sbuf[off...]
   auto stage_all = [&](const double* X, int E, int off) {
@@ -255,21 +255,40 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
     }
     __syncthreads();
     qp_stamp(a, 9);  // diagnostic: G / g0 in registers
-    // round B: CE and ce0 (equality phase), issued now so they land during the Cholesky
-    if (p > 0) {
-      const int np_ = n * p;
-      const int offc = (kQpw * np_ + 127) / 128 * 128;
-      if (offc + kQpw * p <= STAGE) {
-        stage_all(a.CE, np_, 0);
-        stage_all(a.ce0, p, offc);
+    // round B: CE and ce0 (equality phase), landing during the Cholesky, the J build and the
+    // solve.  A full wave issues its span a part per Cholesky row: issued at once, its LDS-DMA
+    // instructions held the wave's issue until most of the data had arrived (the CU's memory
+    // queues fill), which serialised the transfer with the Cholesky.
+    const int npB = n * p;
+    const int offcB = (kQpw * npB + 127) / 128 * 128;
+    const bool stageB = p > 0 && offcB + kQpw * p <= STAGE;
+    auto round_b = [&](int part, int parts) {
+      if (!stageB) return;
+      if (!full) {
+        if (part == 0) {
+          stage_all(a.CE, npB, 0);
+          stage_all(a.ce0, p, offcB);
+        }
+        return;
       }
-    }
+      const int nce = (kQpw * npB + 127) / 128, tot = nce + (kQpw * p + 127) / 128;
+      const int per = (tot + parts - 1) / parts;
+      const double* ce = a.CE + b0 * (int64_t)npB;
+      const double* c0 = a.ce0 + b0 * (int64_t)p;
+      for (int c = part * per; c < min(tot, (part + 1) * per); c++) {
+        if (c < nce)
+          copy_chunk(ce, kQpw * npB, 0, c * 128);
+        else
+          copy_chunk(c0, kQpw * p, offcB, (c - nce) * 128);
+      }
+    };
 #pragma unroll
     for (int i = 0; i < NM; i++)
       if (i < n) c1 += Gr[i][i];
     // cholesky_decomposition (@.text+0x2df0): row-wise, descending-k sums, upper mirrored
 #pragma unroll
     for (int i = 0; i < NM; i++) {
+      round_b(i, NM);  // every lane (the copy is per wave)
       if (i < n && chol_ok) {
         double sum = Gr[i][i];
 #pragma unroll

@@ -52,9 +52,7 @@ if (s[:, 9] > 0).all():
     if (s[:, 10] > 0).all():
         print(f", Cholesky + round-B wait {(s[:, 10] - s[:, 9]).mean():.0f}", end="")
         if (s[:, 11] > 0).all():
-            print(f", CE -> AGPR {(s[:, 11] - s[:, 10]).mean():.0f}, J + solve {(s[:, 1] - s[:, 11]).mean():.0f}", end="")
-        else:
-            print(f", J + solve {(s[:, 1] - s[:, 10]).mean():.0f}", end="")
+            print(f", CE -> AGPR {(s[:, 11] - s[:, 10]).mean():.0f}, warm-up + J + solve {(s[:, 1] - s[:, 11]).mean():.0f}", end="")
     print()
 start = s[:, 0] - s[:, 0].min()
 print("  wave start offsets (cycles): p50", np.median(start), "max", start.max(), " end max", (s[:, 4] - s[:, 0].min()).max())
