@@ -91,6 +91,9 @@ def parse(argv=None):
                          "defeat the Infinity Cache, 1 = warm)")
     ap.add_argument("--kernel-reps", type=int, default=20,
                     help="serialized launches timed for the roofline's kernel duration")
+    ap.add_argument("--fast", action="store_true",
+                    help="QPGPU_FLAG_FAST: the lane kernel's fast build (x, f within 1e-10 of the "
+                         "reference instead of bitwise)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -244,7 +247,7 @@ def main():
         scaling = "weak"
     b0, b1 = qpdist.shard(rank, B)
     pr = qpgpu.make_problems(kind, n, p, m, b0, b1, seed=args.seed)
-    kname = qpgpu.kernel_name(n, p, m)
+    kname = qpgpu.kernel_name(n, p, m, fast=args.fast)
     if args.family:
         kname = {"lane": f"qp_lane[n={n},m={m}]", "subgroup": f"qp_small[n={n},m={m}]",
                  "wave": f"qp_wave[n={n},m={m}]"}[args.family]
@@ -280,7 +283,7 @@ def main():
             v = sets[r].__class__.__new__(sets[r].__class__)
             v.__dict__.update(sets[r].__dict__)
             v.x, v.f, v.status = outs[j]
-            launchers[key] = v.launcher(stream, family=args.family)
+            launchers[key] = v.launcher(stream, family=args.family, fast=args.fast)
         return launchers[key]
 
     gather = world > 1 and not args.no_gather
@@ -387,7 +390,7 @@ def main():
     hb.__dict__.update(base.__dict__)
     hb.x, hb.f, hb.status = (torch.empty_like(t) for t in outs[0])
     hb.iters = torch.zeros(B, dtype=torch.int32, device=dev)
-    hb.launcher(cs, family=args.family)()
+    hb.launcher(cs, family=args.family, fast=args.fast)()
     torch.cuda.synchronize(dev)
     hist = torch.bincount(hb.iters[:B].to(torch.int64).clamp(min=0)).cpu().tolist()
     gpu_sample = None
@@ -484,6 +487,8 @@ def main():
         "data": "synthetic",
         "config": {"workload": desc, "kind": kind, "n": n, "p": p, "m": m, "batch_per_gpu": B,
                    "global_batch": B * world, "kernel": kname, "layout": args.layout,
+                   "arithmetic": ("fast: fused multiply-adds, shared reciprocals; x, f within 1e-10"
+                                  if args.fast else "exact: the reference's operation order, bitwise"),
                    "streams": S, "input_sets": R, "cold_inputs": R > 1 or in_bytes * B >= 2 * MALL_BYTES,
                    "backend": backend if world > 1 else None, "parallelism": par},
         "value_streams1": total / elapsed1,

@@ -99,6 +99,17 @@ enum qpgpu_error {
                                           and iteration counts) instead.  Implied by
                                           QPGPU_FLAG_WRITE_FACTOR. */
 
+#define QPGPU_FLAG_FAST 0x4u          /* shapes the lane kernel serves (n <= 8, m <= 16): run its
+                                          fast build — multiply-adds fused, one refined
+                                          reciprocal per shared divisor, rotation lengths as
+                                          sqrt(a^2 + b^2) inside the exponent range — whose x and
+                                          f match the reference within 1e-10 relative
+                                          (|a - b| / max(1, |b|)) with the same decisions on
+                                          well-conditioned problems, instead of bit for bit.
+                                          Other shapes run as without it.  Not combinable with
+                                          QPGPU_FLAG_EXACT or QPGPU_FLAG_WRITE_FACTOR
+                                          (QPGPU_ERR_INVALID_ARGUMENT). */
+
 /* Kernel-family selection (benchmarking / testing knobs; default = fastest for the shape):
  *   LANE      one QP per lane (qp_lane.hip, n <= 8, m <= 16)
  *   SUBGROUP  one QP per S-lane subgroup, register state (qp_small.hip, n <= 16, m <= 64)
@@ -173,6 +184,9 @@ int qpgpu_max_m(void);
 
 /* Name of the kernel variant qpgpu_solve_batched would launch for this shape ("" if none). */
 const char* qpgpu_kernel_name(int32_t n, int32_t p, int32_t m);
+/* The same for a launch with these QPGPU_FLAG_* flags (QPGPU_FLAG_FAST selects the lane
+ * kernel's fast build where it covers the shape). */
+const char* qpgpu_kernel_name_flags(int32_t n, int32_t p, int32_t m, uint32_t flags);
 
 /* Human-readable text for the last QPGPU_ERR_HIP on this thread. */
 const char* qpgpu_last_error(void);

@@ -107,7 +107,7 @@ struct QpArgs {
   // boundaries, kStampSlots per wave, written by lane 0.  Never feeds an output.
   uint64_t* stamps;
 };
-constexpr int kStampSlots = 16;
+constexpr int kStampSlots = 18;
 // internal QpArgs.flags bit set by the host when CI and ci0 are 16-byte aligned
 constexpr uint32_t kArgAligned16 = 0x80000000u;
 // internal QpArgs.flags bit: the workspace already holds the setup (qp_panel.hip) — J, x0, f0,
@@ -132,6 +132,12 @@ __device__ __forceinline__ void qp_stamp(const QpArgs& a, int slot) {
   if (a.stamps) {
     const uint64_t t = __builtin_amdgcn_s_memtime();
     if (threadIdx.x == 0) a.stamps[(uint64_t)blockIdx.x * kStampSlots + slot] = t;
+    // start / end also on the 100 MHz constant clock (s_memtime is the shader clock of the
+    // wave's XCD, neither constant-rate nor synchronised across XCDs): slots 16 / 17
+    if (slot == 0 || slot == 4) {
+      const uint64_t r = __builtin_amdgcn_s_memrealtime();
+      if (threadIdx.x == 0) a.stamps[(uint64_t)blockIdx.x * kStampSlots + 16 + (slot == 4)] = r;
+    }
   }
 }
 

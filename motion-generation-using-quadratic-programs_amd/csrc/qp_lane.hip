@@ -22,11 +22,33 @@
 //     global loads at all.
 // IEEE binary64 throughout, no contraction: results are bitwise identical to the CPU
 // restatement (oracle/qp_oracle.c), which tests/ check.
+//
+// The same source built a second time with QPGPU_LANE_FAST=1 and -ffp-contract=fast
+// (qp_lane_fast.hip) is the QPGPU_FLAG_FAST kernel: same algorithm and decisions, but multiply-
+// adds fused, every division by a shared divisor a multiplication by one refined reciprocal
+// (Cholesky columns, J = L^-T, the solve, the Givens coefficients), and the rotation length as
+// sqrt(a^2 + b^2) for operands well inside the exponent range — within north_star's 1e-10
+// relative of the reference instead of bit-identical.
 #include <type_traits>
 
 #include "qp_common.h"
 
-namespace qpk {
+#ifndef QPGPU_LANE_FAST
+#define QPGPU_LANE_FAST 0
+#endif
+#if QPGPU_LANE_FAST
+#define QPK_LANE_NS qpk_fast
+#define QP_LANE_KERNEL qp_lane_fast_kernel
+#define QPK_LANE_C(name) name##_fast
+#else
+#define QPK_LANE_NS qpk
+#define QP_LANE_KERNEL qp_lane_kernel
+#define QPK_LANE_C(name) name
+#endif
+
+namespace QPK_LANE_NS {
+using namespace qpk;
+constexpr bool kFast = QPGPU_LANE_FAST != 0;
 
 template <typename T>
 __device__ __forceinline__ T opq_l(T v) {
@@ -103,14 +125,73 @@ constexpr int kScanDepth = 2;
 
 __device__ __forceinline__ bool wave_any(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
 
+// ---- arithmetic of the fast build.  F (= kFast and not the fallback body) selects the fast
+// forms; otherwise a / b is the IEEE division and distance the reference's scaled form.  The
+// fast forms are valid for operands well inside the exponent range: each one ANDs its own
+// validity into the lane's `ok`, and a wave with any lane not ok re-solves with the IEEE forms
+// (lane_body<..., SAFE = true>), so no branch sits inside the arithmetic.
+// 1 / b: the v_rcp_f64 seed and the two Newton steps of the compiler's own division sequence,
+// without its range scaling and special-case fix-up
+__device__ __forceinline__ double frcp(double b) {
+  double y = __builtin_amdgcn_rcp(b);
+  double e = __builtin_fma(-b, y, 1.0);
+  y = __builtin_fma(y, e, y);
+  e = __builtin_fma(-b, y, 1.0);
+  return __builtin_fma(y, e, y);
+}
+__device__ __forceinline__ bool rcp_ok(double r) {
+  return __builtin_amdgcn_class(r, 0x108);  // +-normal (b zero, denormal, huge, inf or NaN fail)
+}
+// a / b given rb = frcp(b) (F) — a * rb
+template <bool F>
+__device__ __forceinline__ double ldiv_r(double a, double b, double rb, bool& ok) {
+  if constexpr (F) {
+    ok = ok && rcp_ok(rb);
+    return a * rb;
+  } else {
+    return a / b;
+  }
+}
+template <bool F>
+__device__ __forceinline__ double ldiv(double a, double b, bool& ok) {
+  if constexpr (F)
+    return ldiv_r<true>(a, b, frcp(b), ok);
+  else
+    return a / b;
+}
+// distance(a, b) (F): sqrt(a^2 + b^2) with the [1, 2]-free form of sqrt_1to2's refinement,
+// valid for a^2 + b^2 in [2^-600, 2^600] (and exactly 0 when a = b = 0, as the reference's)
+template <bool F>
+__device__ __forceinline__ double ldistance(double a, double b, bool& ok) {
+  if constexpr (F) {
+    const double s = __builtin_fma(a, a, b * b);
+    const double y = __builtin_amdgcn_rsq(s);
+    double g = s * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    const double d = __builtin_fma(-g, g, s);
+    g = __builtin_fma(d, h, g);
+    const bool z = (a == 0.0) && (b == 0.0);
+    ok = ok && (z || (s >= 0x1p-600 && s <= 0x1p600));
+    return z ? 0.0 : g;
+  } else {
+    return qp_distance(a, b);
+  }
+}
+
 // PX >= 0: p is the compile-time constant PX as well (C1/C4: 6, C2: 0), which folds every
 // [p, iq) loop of the active-set phase (for n = 7, p = 6 that range holds at most one entry).
-template <int NM, int MM, int T, bool EXACT, int PX>
-__global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
+// The solve of one wave's 64 QPs.  SAFE: the IEEE forms of division and distance (the exact
+// build always; the fast build's fallback).  Returns false, having written nothing, when the
+// fast forms were not valid for some lane (then the caller re-solves with SAFE).
+template <int NM, int MM, int T, bool EXACT, int PX, bool SAFE>
+__device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
   static_assert(MM <= 64, "bitmask bookkeeping holds m <= 64");
   using RI = RIdx<NM>;
   constexpr int STAGE = kStage;
-  __shared__ double sbuf[STAGE];
+  constexpr bool F = kFast && !SAFE;
+  bool fok = true;  // F: every fast form so far was valid on this lane
   // CI / ci0 cache warm-up before the equality phase: only with an equality phase long enough
   // for the loads to land (p > 0 or p unknown).  Measured for p = 0 (no equality phase): the
   // first scan then waits on the same burst either way (profiles/r02_s2, r02_s46).
@@ -299,13 +380,14 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
         } else {
           const double dg = sqrt(sum);
           Gr[i][i] = dg;
+          const double rdg = F ? frcp(dg) : 0.0;
 #pragma unroll
           for (int j = i + 1; j < NM; j++)
             if (j < n) {
               double s2 = Gr[i][j];
 #pragma unroll
               for (int k = i - 1; k >= 0; k--) s2 -= Gr[i][k] * Gr[j][k];
-              Gr[j][i] = s2 / dg;
+              Gr[j][i] = ldiv_r<F>(s2, dg, rdg, fok);
             }
 #pragma unroll
           for (int k = i + 1; k < NM; k++) Gr[i][k] = Gr[k][i];
@@ -361,6 +443,10 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
 #pragma unroll
         for (int j = 0; j <= i; j++)
           if (i < n) lfin = lfin && (fabs(Gr[i][j]) < inf);
+      // fast build: one reciprocal per pivot serves the J build and the solve
+      double rdiag[NM];
+#pragma unroll
+      for (int i = 0; i < NM; i++) rdiag[i] = (F && i < n) ? frcp(Gr[i][i]) : 0.0;
       auto build_j = [&](const bool skip) {
 #pragma unroll
         for (int r = 0; r < NM; r++) {
@@ -373,7 +459,7 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
 #pragma unroll
               for (int j = 0; j < i; j++)
                 if (!(skip && j < r)) v -= Gr[i][j] * y[j];
-              v = v / Gr[i][i];
+              v = ldiv_r<F>(v, Gr[i][i], rdiag[i], fok);
             }
             y[i] = v;
           }
@@ -382,7 +468,9 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
           if (r < n) c2 += y[r];
         }
       };
-      if (lfin)
+      // (fast build: the skipping form unless some lane's factor is non-finite, decided per
+      // wave so that the two forms stay separate code)
+      if (F ? !wave_any(!lfin) : lfin)
         build_j(true);
       else
         build_j(false);
@@ -395,7 +483,7 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
           v = g0v[i];
 #pragma unroll
           for (int j = 0; j < i; j++) v -= Gr[i][j] * y[j];
-          v = v / Gr[i][i];
+          v = ldiv_r<F>(v, Gr[i][i], rdiag[i], fok);
         }
         y[i] = v;
       }
@@ -406,7 +494,7 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
 #pragma unroll
           for (int j = i + 1; j < NM; j++)
             if (j < n) v -= Gr[i][j] * xv[j];
-          xv[i] = v / Gr[i][i];
+          xv[i] = ldiv_r<F>(v, Gr[i][i], rdiag[i], fok);
         }
       }
 #pragma unroll
@@ -487,9 +575,35 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
 #pragma unroll
         for (int j = i + 1; j < NM; j++)
           if (j < LO || j < iq) s += Rv[RI::at(i, j)] * rv[j];
-        rv[i] = (dv[i] - s) / Rv[RI::at(i, i)];
+        rv[i] = ldiv<F>(dv[i] - s, Rv[RI::at(i, i)], fok);
       }
     }
+  };
+  // Fast build: the Givens step of add_constraint / delete_constraint without a branch.  The
+  // pair (a, b) -> (+-h, 0) with h = |(a, b)| and the sign of a (the reference's cc < 0 test,
+  // h > 0); the rows (t1, t2) -> (cc t1 + ss t2, ss t1 - cc t2), which is the reference's
+  // xny (t1 + n1) - t2 with xny = ss / (1 + cc) and ss^2 + cc^2 = 1, without that division.  When
+  // |h| < eps the reference skips the rotation: the coefficients become (1, 0 | 0, -1), the
+  // identity, and (a, b) stay — so the step is straight-line code the scheduler can overlap with
+  // the next rotation's h chain (which needs only +-h, not the coefficients).
+  auto rot_fast = [&](double& a_, double& b_, auto&& apply) {
+    const double a0 = a_, b0 = b_;
+    const double h = ldistance<true>(a0, b0, fok);
+    const bool skip = fabs(h) < kEps;
+    const double rh = frcp(h);
+    fok = fok && (skip || rcp_ok(rh));
+    const bool neg = a0 < 0.0;
+    const double cc = fabs(a0) * rh;
+    const double ss = (neg ? -b0 : b0) * rh;
+    a_ = skip ? a0 : (neg ? -h : h);
+    b_ = skip ? b0 : 0.0;
+    const double c1_ = skip ? 1.0 : cc, s1_ = skip ? 0.0 : ss;
+    const double c2_ = skip ? -1.0 : cc, s2_ = skip ? 0.0 : ss;
+    apply([&](double& t1r, double& t2r) {
+      const double t1 = t1r, t2 = t2r;
+      t1r = c1_ * t1 + s1_ * t2;
+      t2r = s2_ * t1 - c2_ * t2;
+    });
   };
   // LoC: a compile-time lower bound on iq (std::integral_constant).  In the active-set loop
   // iq >= p always (equality constraints are never dropped), so entries below p of R, A, u and
@@ -501,12 +615,21 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
 #pragma unroll
     for (int j = NM - 1; j >= LO + 1; j--) {
       if (j <= n - 1 && j >= iq + 1) {
+        if constexpr (F) {
+          rot_fast(dv[j - 1], dv[j], [&](auto&& rot) {
+#pragma unroll
+            for (int k = 0; k < NM; k++)
+              if (k < n) rot(Jreg[k][j - 1], Jreg[k][j]);
+          });
+          continue;
+        }
         double cc = dv[j - 1], ss = dv[j];
-        const double h = qp_distance(cc, ss);
+        const double h = ldistance<F>(cc, ss, fok);
         if (!(fabs(h) < kEps)) {
           dv[j] = 0.0;
-          ss = ss / h;
-          cc = cc / h;
+          const double rh = F ? frcp(h) : 0.0;
+          ss = ldiv_r<F>(ss, h, rh, fok);
+          cc = ldiv_r<F>(cc, h, rh, fok);
           if (cc < 0.0) {
             cc = -cc;
             ss = -ss;
@@ -514,7 +637,7 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
           } else {
             dv[j - 1] = h;
           }
-          const double xny = ss / (1.0 + cc);
+          const double xny = ldiv<F>(ss, 1.0 + cc, fok);
 #pragma unroll
           for (int k = 0; k < NM; k++)
             if (k < n) {
@@ -587,11 +710,23 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
 #pragma unroll
     for (int j = LO; j < NM - 1; j++) {
       if (j >= qq && j < iq) {
+        if constexpr (F) {
+          rot_fast(Rv[RI::at(j, j)], Rv[RI::at(j + 1, j)], [&](auto&& rot) {
+#pragma unroll
+            for (int k = j + 1; k < NM; k++)
+              if (k < iq) rot(Rv[RI::at(j, k)], Rv[RI::at(j + 1, k)]);
+#pragma unroll
+            for (int k = 0; k < NM; k++)
+              if (k < n) rot(Jreg[k][j], Jreg[k][j + 1]);
+          });
+          continue;
+        }
         double cc = Rv[RI::at(j, j)], ss = Rv[RI::at(j + 1, j)];
-        const double h = qp_distance(cc, ss);
+        const double h = ldistance<F>(cc, ss, fok);
         if (!(fabs(h) < kEps)) {
-          cc = cc / h;
-          ss = ss / h;
+          const double rh = F ? frcp(h) : 0.0;
+          cc = ldiv_r<F>(cc, h, rh, fok);
+          ss = ldiv_r<F>(ss, h, rh, fok);
           Rv[RI::at(j + 1, j)] = 0.0;
           if (cc < 0.0) {
             Rv[RI::at(j, j)] = -h;
@@ -600,7 +735,7 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
           } else {
             Rv[RI::at(j, j)] = h;
           }
-          const double xny = ss / (1.0 + cc);
+          const double xny = ldiv<F>(ss, 1.0 + cc, fok);
 #pragma unroll
           for (int k = j + 1; k < NM; k++)
             if (k < iq) {
@@ -688,7 +823,7 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
       double t2 = 0.0;
       const double zz = dot(zv, zv);
       const double znp = dot(zv, npv);
-      if (fabs(zz) > kEps) t2 = (-dot(npv, xv) - c0) / znp;
+      if (fabs(zz) > kEps) t2 = ldiv<F>(-dot(npv, xv) - c0, znp, fok);
 #pragma unroll
       for (int k = 0; k < NM; k++) xv[k] += t2 * zv[k];
       uv[i < NM + 1 ? i : NM] = t2;
@@ -989,7 +1124,7 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
 #pragma unroll
           for (int k = 0; k < NM; k++)
             if (k >= p && k < iq && rv[k] > 0.0) {
-              const double q_ = uv[k] / rv[k];
+              const double q_ = ldiv<F>(uv[k], rv[k], fok);
               const bool take = q_ < t1;
               t1 = take ? q_ : t1;
               l = take ? opq_l(Av[k]) : l;
@@ -998,7 +1133,7 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
           const double znp = dot(zv, npv);
           double t2;
           if (fabs(zz) > kEps) {
-            t2 = -lsel<MM>(sv, ip) / znp;
+            t2 = ldiv<F>(-lsel<MM>(sv, ip), znp, fok);
             if (t2 < 0) t2 = inf;  // Takano Akio patch
           } else {
             t2 = inf;
@@ -1066,6 +1201,9 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
     }
   }
   qp_stamp(a, 3);
+  if constexpr (F) {
+    if (wave_any(!fok)) return false;
+  }
 
   if (live) {
     if (chol_ok) {
@@ -1079,6 +1217,20 @@ __global__ void __launch_bounds__(64, 1) qp_lane_kernel(const QpArgs a) {
     if (a.iters) a.iters[b] = iter;
   }
   qp_stamp(a, 4);
+  return true;
+}
+
+template <int NM, int MM, int T, bool EXACT, int PX>
+__global__ void __launch_bounds__(64, 1) QP_LANE_KERNEL(const QpArgs a) {
+  __shared__ double sbuf[kStage];
+  if constexpr (kFast) {
+    if (!lane_body<NM, MM, T, EXACT, PX, false>(a, sbuf)) {
+      __syncthreads();  // the fast attempt's LDS traffic is over
+      lane_body<NM, MM, T, EXACT, PX, true>(a, sbuf);
+    }
+  } else {
+    lane_body<NM, MM, T, EXACT, PX, true>(a, sbuf);
+  }
 }
 
 template <int NM, int MM, int T>
@@ -1087,13 +1239,13 @@ static void launch_lane_t(const QpArgs& a, hipStream_t stream) {
   const dim3 g((unsigned)blocks), blk(64);
   if (a.n == NM && a.m == MM && !a.x_eq) {
     if (a.p == 6)
-      hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, true, 6>), g, blk, 0, stream, a);
+      hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, 6>), g, blk, 0, stream, a);
     else if (a.p == 0)
-      hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, true, 0>), g, blk, 0, stream, a);
+      hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, 0>), g, blk, 0, stream, a);
     else
-      hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, true, -1>), g, blk, 0, stream, a);
+      hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, -1>), g, blk, 0, stream, a);
   } else {
-    hipLaunchKernelGGL((qp_lane_kernel<NM, MM, T, false, -1>), g, blk, 0, stream, a);
+    hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, false, -1>), g, blk, 0, stream, a);
   }
 }
 
@@ -1113,8 +1265,8 @@ struct LaneVariant {
 };
 
 static const LaneVariant kLaneVariants[] = {
-    {7, 14, "qp_lane<N=7,M=14>", launch_lane<7, 14>},
-    {8, 16, "qp_lane<N=8,M=16>", launch_lane<8, 16>},
+    {7, 14, kFast ? "qp_lane_fast<N=7,M=14>" : "qp_lane<N=7,M=14>", launch_lane<7, 14>},
+    {8, 16, kFast ? "qp_lane_fast<N=8,M=16>" : "qp_lane<N=8,M=16>", launch_lane<8, 16>},
 };
 
 const LaneVariant* pick_lane(int n, int m) {
@@ -1123,11 +1275,11 @@ const LaneVariant* pick_lane(int n, int m) {
   return nullptr;
 }
 
-}  // namespace qpk
+}  // namespace QPK_LANE_NS
 
-extern "C" hipError_t qpk_launch_lane(const qpk::QpArgs* a, hipStream_t stream, int* handled,
-                                      const char** name) {
-  const qpk::LaneVariant* v = qpk::pick_lane(a->n, a->m);
+extern "C" hipError_t QPK_LANE_C(qpk_launch_lane)(const qpk::QpArgs* a, hipStream_t stream, int* handled,
+                                                  const char** name) {
+  const QPK_LANE_NS::LaneVariant* v = QPK_LANE_NS::pick_lane(a->n, a->m);
   if (!v) {
     *handled = 0;
     return hipSuccess;
@@ -1137,7 +1289,7 @@ extern "C" hipError_t qpk_launch_lane(const qpk::QpArgs* a, hipStream_t stream, 
   return v->launch(*a, stream);
 }
 
-extern "C" const char* qpk_lane_name(int n, int /*p*/, int m) {
-  const qpk::LaneVariant* v = qpk::pick_lane(n, m);
+extern "C" const char* QPK_LANE_C(qpk_lane_name)(int n, int /*p*/, int m) {
+  const QPK_LANE_NS::LaneVariant* v = QPK_LANE_NS::pick_lane(n, m);
   return v ? v->name : nullptr;
 }

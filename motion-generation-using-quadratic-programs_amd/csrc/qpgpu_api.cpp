@@ -21,6 +21,9 @@ extern "C" const char* qpk_small_name(int n, int p, int m);
 extern "C" hipError_t qpk_launch_lane(const qpk::QpArgs* a, hipStream_t stream, int* handled,
                                       const char** name);
 extern "C" const char* qpk_lane_name(int n, int p, int m);
+extern "C" hipError_t qpk_launch_lane_fast(const qpk::QpArgs* a, hipStream_t stream, int* handled,
+                                           const char** name);
+extern "C" const char* qpk_lane_name_fast(int n, int p, int m);
 extern "C" hipError_t qpk_launch_medium_ws(const qpk::QpArgs* a, hipStream_t stream, int* handled,
                                            const char** name, double* ws);
 extern "C" int64_t qpk_medium_workspace_bytes(int n, int m, int64_t batch);
@@ -51,8 +54,10 @@ int validate(const qpgpu_problem_desc* d) {
   if (d->layout != QPGPU_LAYOUT_QP_MAJOR && d->layout != QPGPU_LAYOUT_TILED64)
     return QPGPU_ERR_INVALID_ARGUMENT;
   const uint32_t fam = QPGPU_FLAG_FORCE_LANE | QPGPU_FLAG_FORCE_SUBGROUP | QPGPU_FLAG_FORCE_WAVE;
-  const uint32_t known = QPGPU_FLAG_WRITE_FACTOR | QPGPU_FLAG_EXACT | fam;
+  const uint32_t known = QPGPU_FLAG_WRITE_FACTOR | QPGPU_FLAG_EXACT | QPGPU_FLAG_FAST | fam;
   if (d->flags & ~known) return QPGPU_ERR_INVALID_ARGUMENT;
+  if ((d->flags & QPGPU_FLAG_FAST) && (d->flags & (QPGPU_FLAG_EXACT | QPGPU_FLAG_WRITE_FACTOR)))
+    return QPGPU_ERR_INVALID_ARGUMENT;
   const uint32_t f = d->flags & fam;
   if (f & (f - 1)) return QPGPU_ERR_INVALID_ARGUMENT;  // at most one family
   return QPGPU_SUCCESS;
@@ -133,6 +138,14 @@ int qpgpu_max_m(void) {
 // 2.2 vs 3.5 ms) and at m = 64; the S = 8 subgroup kernel still wins at n <= 8, m <= 32.
 static bool default_small(int n, int m) { return n <= 8 && m <= 32; }
 
+const char* qpgpu_kernel_name_flags(int32_t n, int32_t p, int32_t m, uint32_t flags) {
+  if ((flags & QPGPU_FLAG_FAST) && !(flags & (QPGPU_FLAG_FORCE_SUBGROUP | QPGPU_FLAG_FORCE_WAVE)) && n > 0 && p >= 0 && m >= 0) {
+    const char* s = qpk_lane_name_fast(n, p, m);
+    if (s) return s;
+  }
+  return qpgpu_kernel_name(n, p, m);
+}
+
 const char* qpgpu_kernel_name(int32_t n, int32_t p, int32_t m) {
   if (n <= 0 || p < 0 || m < 0) return "";
   const char* s = qpk_lane_name(n, p, m);
@@ -204,6 +217,10 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
   int handled = 0;
   hipError_t e = hipSuccess;
   a.flags = d->flags & (QPGPU_FLAG_WRITE_FACTOR | QPGPU_FLAG_EXACT);
+  const bool fast = (d->flags & QPGPU_FLAG_FAST) != 0;
+  auto launch_lane = [&]() {
+    return fast ? qpk_launch_lane_fast(&a, s, &handled, nullptr) : qpk_launch_lane(&a, s, &handled, nullptr);
+  };
   if (((reinterpret_cast<uintptr_t>(CI) | reinterpret_cast<uintptr_t>(ci0)) & 15u) == 0)
     a.flags |= qpk::kArgAligned16;
   auto launch_wave = [&]() -> int {
@@ -215,13 +232,13 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
   };
   int wrc = QPGPU_SUCCESS;
   if (d->flags & QPGPU_FLAG_FORCE_LANE) {
-    e = qpk_launch_lane(&a, s, &handled, nullptr);
+    e = launch_lane();
   } else if (d->flags & QPGPU_FLAG_FORCE_SUBGROUP) {
     e = qpk_launch_small(&a, s, &handled, nullptr);
   } else if (d->flags & QPGPU_FLAG_FORCE_WAVE) {
     wrc = launch_wave();
   } else {
-    e = qpk_launch_lane(&a, s, &handled, nullptr);
+    e = launch_lane();
     if (!handled && default_small(a.n, a.m)) e = qpk_launch_small(&a, s, &handled, nullptr);
     if (!handled) wrc = launch_wave();
   }

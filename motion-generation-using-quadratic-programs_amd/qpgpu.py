@@ -45,6 +45,7 @@ ERR_NO_DEVICE = 4
 
 FLAG_WRITE_FACTOR = 0x1
 FLAG_EXACT = 0x2  # reference operation order for n > 64 too (no MFMA panel setup)
+FLAG_FAST = 0x4  # lane-kernel shapes: fused multiply-adds, shared reciprocals (1e-10, not bitwise)
 FLAG_FORCE_LANE = 0x100
 FLAG_FORCE_SUBGROUP = 0x200
 FLAG_FORCE_WAVE = 0x400
@@ -61,6 +62,7 @@ EXPORTED_SYMBOLS = (
     "qpgpu_max_n",
     "qpgpu_max_m",
     "qpgpu_kernel_name",
+    "qpgpu_kernel_name_flags",
     "qpgpu_last_error",
     "qpgpu_device_count",
     "qpgpu_abi_version",
@@ -99,6 +101,8 @@ def _load():
     lib.qpgpu_solve_batched_host.restype = ctypes.c_int
     lib.qpgpu_kernel_name.argtypes = [ctypes.c_int32] * 3
     lib.qpgpu_kernel_name.restype = ctypes.c_char_p
+    lib.qpgpu_kernel_name_flags.argtypes = [ctypes.c_int32] * 3 + [ctypes.c_uint32]
+    lib.qpgpu_kernel_name_flags.restype = ctypes.c_char_p
     lib.qpgpu_last_error.restype = ctypes.c_char_p
     lib.qpgpu_max_n.restype = ctypes.c_int
     lib.qpgpu_max_m.restype = ctypes.c_int
@@ -112,7 +116,9 @@ def _load():
 LIB = _load()
 
 
-def kernel_name(n: int, p: int, m: int) -> str:
+def kernel_name(n: int, p: int, m: int, fast: bool = False) -> str:
+    if fast:
+        return LIB.qpgpu_kernel_name_flags(n, p, m, FLAG_FAST).decode()
     return LIB.qpgpu_kernel_name(n, p, m).decode()
 
 
@@ -187,15 +193,16 @@ def algorithmic_bytes_per_qp(n: int, p: int, m: int) -> int:
 # host-pointer solve (numpy in, numpy out) — copies through the C-ABI's host entry point
 # ----------------------------------------------------------------------------------------------
 def solve_batched_host(pr: Problems, write_factor: bool = False, max_iter: int = 0, family=None,
-                       layout=None, exact: bool = False):
+                       layout=None, exact: bool = False, fast: bool = False):
     """Solve every QP of `pr` on the GPU.  Returns (x, f, status, iters).
 
     With write_factor=True, pr.G is overwritten with each QP's Cholesky factor, as the
     reference overwrites G (QuadProg++.hh:42-45).  layout="tiled64" sends the batch in the
     TILED64 layout (converted here on the host) and converts x / G back.  exact=True keeps the
-    reference's operation order for n > 64 as well (QPGPU_FLAG_EXACT)."""
+    reference's operation order for n > 64 as well (QPGPU_FLAG_EXACT); fast=True runs the lane
+    kernel's fast build (QPGPU_FLAG_FAST: within 1e-10, not bitwise)."""
     B, n, p, m = pr.batch, pr.n, pr.p, pr.m
-    xflags = FAMILY_FLAGS[family] | (FLAG_EXACT if exact else 0)
+    xflags = FAMILY_FLAGS[family] | (FLAG_EXACT if exact else 0) | (FLAG_FAST if fast else 0)
     if LAYOUTS[layout] == LAYOUT_TILED64:
         arrs = [to_tiled64(np.asarray(a, dtype=np.float64)) for a in pr.arrays()]
         xt = np.zeros((B + 63) // 64 * 64 * n, dtype=np.float64)
@@ -247,7 +254,7 @@ class DeviceBatch:
         self.iters = torch.zeros(self.batch, dtype=torch.int32, device=device) if with_iters else None
 
     def solve(self, stream=None, max_iter: int = 0, write_factor: bool = False, family=None,
-              eq_out=None, exact: bool = False):
+              eq_out=None, exact: bool = False, fast: bool = False):
         """Enqueue one batched solve on `stream` (a torch.cuda.Stream, default current).
         eq_out=(x_eq, f_eq, status_eq) tensors also receive the m = 0 answer
         (qpgpu_solve_batched_eq)."""
@@ -257,7 +264,7 @@ class DeviceBatch:
             stream = torch.cuda.current_stream(self.x.device)
         d = ProblemDesc(self.n, self.p, self.m, max_iter, self.batch,
                         (FLAG_WRITE_FACTOR if write_factor else 0) | FAMILY_FLAGS[family]
-                        | (FLAG_EXACT if exact else 0), self.layout)
+                        | (FLAG_EXACT if exact else 0) | (FLAG_FAST if fast else 0), self.layout)
         vp = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
         args = [ctypes.byref(d), vp(self.G), vp(self.g0), vp(self.CE), vp(self.ce0), vp(self.CI),
                 vp(self.ci0), vp(self.x), vp(self.f), vp(self.status), vp(self.iters)]
@@ -268,11 +275,12 @@ class DeviceBatch:
                                             ctypes.c_void_p(stream.cuda_stream))
         _check(rc, "qpgpu_solve_batched")
 
-    def launcher(self, stream, max_iter: int = 0, family=None, exact: bool = False):
+    def launcher(self, stream, max_iter: int = 0, family=None, exact: bool = False, fast: bool = False):
         """A zero-argument callable that enqueues this batch's solve on `stream` with every ctypes
         argument prebuilt (for tight launch loops: ~2 us of host time per launch)."""
         d = ProblemDesc(self.n, self.p, self.m, max_iter, self.batch,
-                        FAMILY_FLAGS[family] | (FLAG_EXACT if exact else 0), self.layout)
+                        FAMILY_FLAGS[family] | (FLAG_EXACT if exact else 0) | (FLAG_FAST if fast else 0),
+                        self.layout)
         vp = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
         args = (ctypes.byref(d), vp(self.G), vp(self.g0), vp(self.CE), vp(self.ce0), vp(self.CI),
                 vp(self.ci0), vp(self.x), vp(self.f), vp(self.status), vp(self.iters),

@@ -295,3 +295,60 @@ def test_c5_bench_problems_parity(gpu, exact):
         pr = qpgpu.make_problems("general", n, p, m, b0, b0 + 3, seed=2026)
         so, io = assert_parity(pr, f"C5 bench QPs {b0}..{b0 + 2}", exact=exact)
         assert (so == qpgpu.QP_OK).all() and io.min() > 50, (so, io)
+
+
+# ---- QPGPU_FLAG_FAST (the lane kernel's fast build): north_star's 1e-10 on x and f,
+# same status and l1-pass counts, on every shape the lane kernel covers
+
+def assert_fast_parity(pr, label, layout=None, decisions=True):
+    prc = qpgpu.Problems(pr.n, pr.p, pr.m, pr.G.copy(), pr.g0, pr.CE, pr.ce0, pr.CI, pr.ci0)
+    xo, fo, so, io = oracle.solve_batch(prc, max_steps=1000 + 100 * (pr.n + pr.p + pr.m))
+    xg, fg, sg, ig = qpgpu.solve_batched_host(pr, fast=True, layout=layout)
+    assert np.array_equal(so, sg), f"{label}: status differs at {np.where(so != sg)[0][:10]}"
+    if decisions:
+        assert np.array_equal(io, ig), f"{label}: l1-pass count differs at {np.where(io != ig)[0][:10]}"
+    ok = so == qpgpu.QP_OK
+    ex, ef = _relerr(xg[ok], xo[ok]), _relerr(fg[ok], fo[ok])
+    assert ex <= TOL and ef <= TOL, f"{label}: rel err x {ex:.3e} f {ef:.3e}"
+    return ex, ef
+
+
+@pytest.mark.parametrize("layout", ["qp_major", "tiled64"])
+@pytest.mark.parametrize("kind,p", [("general", 6), ("box", 0)])
+def test_fast_full_size(gpu, kind, p, layout):
+    """C1 / C2 at the bench size (65 536 QPs, seeds 2026 and 12345)."""
+    for seed in (2026, 12345):
+        assert_fast_parity(qpgpu.make_problems(kind, 7, p, 14, 0, 65536, seed=seed), f"fast {kind} {seed}",
+                           layout=layout)
+
+
+@pytest.mark.parametrize("n,p,m", [(7, 3, 14), (8, 2, 16), (5, 1, 9), (3, 0, 6), (8, 0, 16), (7, 6, 10)])
+def test_fast_other_lane_shapes(gpu, n, p, m):
+    """The generic (run-time p) and the N=8 instantiations of the fast build, odd batch sizes."""
+    assert_fast_parity(qpgpu.make_problems("general", n, p, m, 0, 1001, seed=n * 100 + m), f"fast {(n, p, m)}")
+
+
+@pytest.mark.parametrize("name,pr", qp_cases.edge_cases(), ids=[c[0] for c in qp_cases.edge_cases()])
+def test_fast_edge_cases(gpu, name, pr):
+    """Every exit of the algorithm through the fast build: same status; x, f within 1e-10 where the
+    QP is solved.  Non-finite data (the -inf / NaN limits) makes the fast forms invalid on those
+    lanes, so their waves re-solve with IEEE divisions (lane_body<..., SAFE>)."""
+    if not covers("lane", pr.n, pr.m):
+        pytest.skip("shape outside the lane kernel")
+    assert_fast_parity(pr, f"fast {name}")
+
+
+def test_fast_flag_rules(gpu):
+    """FAST does not combine with EXACT or WRITE_FACTOR; outside the lane shapes it is the
+    default path (bitwise)."""
+    pr = qpgpu.make_problems("general", 7, 6, 14, 0, 64, seed=1)
+    with pytest.raises(RuntimeError):
+        qpgpu.solve_batched_host(pr, fast=True, exact=True)
+    with pytest.raises(RuntimeError):
+        qpgpu.solve_batched_host(pr, fast=True, write_factor=True)
+    assert qpgpu.kernel_name(7, 6, 14, fast=True).startswith("qp_lane_fast")
+    assert qpgpu.kernel_name(30, 6, 60, fast=True) == qpgpu.kernel_name(30, 6, 60)
+    big = qp_cases.make("general", 30, 6, 60, 64)
+    xf, ff, sf, _ = qpgpu.solve_batched_host(big, fast=True)
+    xd, fd, sd, _ = qpgpu.solve_batched_host(big)
+    assert np.array_equal(xf.view(np.uint64), xd.view(np.uint64)) and np.array_equal(sf, sd)

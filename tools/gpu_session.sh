@@ -71,6 +71,16 @@ for s in $STEPS; do
     benchcold)
       for c in C1 C2 mgqp C3; do run benchcold_$c 600 python bench.py --config $c --no-cpu --steps 20; done
       run benchcold_C5 600 python bench.py --config C5 --no-cpu --steps 3 --warmup 1 --kernel-reps 3 ;;
+    fastcheck)
+      # the QPGPU_FLAG_FAST lane build: parity against the oracle (1e-10, decisions), then C1 / C2
+      # benches of both builds on the same box
+      run fastdiag 600 python tools/fast_diag.py --fast C1 C2
+      run stamps_fast 300 python tools/stamps.py general qp_major fast
+      run stamps_exact 300 python tools/stamps.py general qp_major
+      for c in ${CONFIGS:-C1 C2}; do
+        run bench_${c}_exact 600 python bench.py --config $c --no-cpu --steps ${ABSTEPS:-30}
+        run bench_${c}_fast 600 python bench.py --config $c --no-cpu --fast --steps ${ABSTEPS:-30}
+      done ;;
     latency)
       run latency 300 tools/dropin_latency 2000 500 ;;
     ab)

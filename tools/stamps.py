@@ -15,25 +15,26 @@ import qpgpu  # noqa: E402
 
 kind, n, p, m = (sys.argv[1] if len(sys.argv) > 1 else "general"), 7, 6, 14
 layout = sys.argv[2] if len(sys.argv) > 2 else "qp_major"
+fast = len(sys.argv) > 3 and sys.argv[3] == "fast"
 if kind == "box":
     p = 0
 B = 65536
 pr = qpgpu.make_problems(kind, n, p, m, 0, B, seed=2026)
 db = qpgpu.DeviceBatch(pr, "cuda:0", layout=layout)
 waves = (B + 63) // 64
-st = torch.zeros(waves * 16, dtype=torch.int64, device="cuda:0")
+st = torch.zeros(waves * 18, dtype=torch.int64, device="cuda:0")
 fn = qpgpu.LIB.qpgpu_debug_set_stamps
 fn.argtypes = [ctypes.c_void_p]
 for rep in range(3):
     fn(ctypes.c_void_p(st.data_ptr()))
-    db.solve(family="lane")
+    db.solve(family="lane", fast=fast)
     torch.cuda.synchronize()
 fn(None)
-s = st.cpu().numpy().reshape(waves, 16).astype(np.int64)
+s = st.cpu().numpy().reshape(waves, 18).astype(np.int64)
 it = db.iters.cpu().numpy()[: waves * 64].reshape(waves, 64)
 names = ["loads+setup", "equality", "active-set", "stores"]
 tot = s[:, 4] - s[:, 0]
-print(f"{kind} {layout}: total cycles/wave mean {tot.mean():.0f} p50 {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max()}")
+print(f"{kind} {layout}{' fast' if fast else ''}: total cycles/wave mean {tot.mean():.0f} p50 {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max()}")
 for k, nm in enumerate(names):
     d = s[:, k + 1] - s[:, k]
     print(f"  {nm:12s} mean {d.mean():9.0f} p50 {np.median(d):9.0f} p90 {np.percentile(d, 90):9.0f} max {d.max():9d}")
@@ -54,5 +55,17 @@ if (s[:, 9] > 0).all():
         if (s[:, 11] > 0).all():
             print(f", CE -> AGPR {(s[:, 11] - s[:, 10]).mean():.0f}, warm-up + J + solve {(s[:, 1] - s[:, 11]).mean():.0f}", end="")
     print()
-start = s[:, 0] - s[:, 0].min()
-print("  wave start offsets (cycles): p50", np.median(start), "max", start.max(), " end max", (s[:, 4] - s[:, 0].min()).max())
+# constant 100 MHz clock (slots 16 / 17): shader clock rate and the spread of wave starts / ends
+rt0, rt1 = s[:, 16], s[:, 17]
+if (rt1 > rt0).all():
+    ghz = (s[:, 4] - s[:, 0]) / ((rt1 - rt0) * 10.0)
+    t0 = rt0.min()
+    st_us, en_us = (rt0 - t0) / 100.0, (rt1 - t0) / 100.0
+    print(f"  shader clock GHz: mean {ghz.mean():.3f} min {ghz.min():.3f} max {ghz.max():.3f}")
+    print(f"  wave start (us after the first): p50 {np.median(st_us):.2f} p90 {np.percentile(st_us, 90):.2f} max {st_us.max():.2f}")
+    print(f"  wave end   (us after the first start): p50 {np.median(en_us):.2f} p90 {np.percentile(en_us, 90):.2f} max {en_us.max():.2f}")
+    dur = en_us - st_us
+    print(f"  wave duration us: mean {dur.mean():.2f} p50 {np.median(dur):.2f} max {dur.max():.2f}")
+    for x in range(8):
+        sel = (np.arange(waves) % 8) == x
+        print(f"    block%8={x}: start max {st_us[sel].max():.2f} end max {en_us[sel].max():.2f} clock {ghz[sel].mean():.3f}")

@@ -21,7 +21,7 @@ n, p, m, B = (int(v) for v in (sys.argv[1:5] if len(sys.argv) >= 5 else (30, 6, 
 pr = qpgpu.make_problems("general", n, p, m, 0, B, seed=2026)
 db = qpgpu.DeviceBatch(pr, "cuda:0")
 blocks = B  # upper bound on blocks (>= QPs / QPs-per-block)
-st = torch.zeros(blocks * 16, dtype=torch.int64, device="cuda:0")
+st = torch.zeros(blocks * 18, dtype=torch.int64, device="cuda:0")
 fn = qpgpu.LIB.qpgpu_debug_set_stamps
 fn.argtypes = [ctypes.c_void_p]
 for rep in range(2):
@@ -30,7 +30,7 @@ for rep in range(2):
     db.solve(family="wave")
     torch.cuda.synchronize()
 fn(None)
-s = st.cpu().numpy().reshape(blocks, 16).astype(np.int64)
+s = st.cpu().numpy().reshape(blocks, 18).astype(np.int64)
 s = s[s[:, 0] != 0]
 names = ["loads+cholesky", "J + x0", "equality", "active-set"]
 tot = s[:, 4] - s[:, 0]
