@@ -91,14 +91,21 @@ def parse(argv=None):
                          "defeat the Infinity Cache, 1 = warm)")
     ap.add_argument("--kernel-reps", type=int, default=20,
                     help="serialized launches timed for the roofline's kernel duration")
+    ap.add_argument("--exact", action="store_true",
+                    help="the bitwise build of the lane kernel (the reference's operation order) "
+                         "instead of QPGPU_FLAG_FAST; the line reports the other one beside it")
     ap.add_argument("--fast", action="store_true",
-                    help="QPGPU_FLAG_FAST: the lane kernel's fast build (x, f within 1e-10 of the "
-                         "reference instead of bitwise)")
+                    help="QPGPU_FLAG_FAST (the default): the lane kernel's fast build, x and f "
+                         "within north_star's 1e-10 of the reference with the same decisions")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--ops-json", default=os.path.join(ROOT, "profiles", "op_counts.json"))
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.exact and args.fast:
+        ap.error("--exact and --fast exclude each other")
+    args.fast = not args.exact
+    return args
 
 
 def _free_port():
@@ -277,13 +284,14 @@ def main():
 
     launchers = {}
 
-    def launcher(r, j, stream):
-        key = (r, j, stream.cuda_stream)
+    def launcher(r, j, stream, fast=None):
+        fast = args.fast if fast is None else fast
+        key = (r, j, stream.cuda_stream, fast)
         if key not in launchers:
             v = sets[r].__class__.__new__(sets[r].__class__)
             v.__dict__.update(sets[r].__dict__)
             v.x, v.f, v.status = outs[j]
-            launchers[key] = v.launcher(stream, family=args.family, fast=args.fast)
+            launchers[key] = v.launcher(stream, family=args.family, fast=fast)
         return launchers[key]
 
     gather = world > 1 and not args.no_gather
@@ -356,11 +364,11 @@ def main():
     # that stream around each launch, rotating over the cold sets (and once more warm)
     cs = streams[0]
 
-    def kernel_ms(rotate, per_launch=False):
+    def kernel_ms(rotate, per_launch=False, fast=None):
         # one HIP-event pair around kernel_reps back-to-back launches on one stream (average
         # launch-to-launch duration: kernel + the dependent-launch gap), or a pair per launch
         K_ = args.kernel_reps
-        fns = [launcher(q % R if rotate else 0, 0, cs) for q in range(K_)]
+        fns = [launcher(q % R if rotate else 0, 0, cs, fast) for q in range(K_)]
         if per_launch:
             st_ = [torch.cuda.Event(enable_timing=True) for _ in range(K_)]
             en_ = [torch.cuda.Event(enable_timing=True) for _ in range(K_)]
@@ -381,6 +389,30 @@ def main():
     kern_cold = kernel_ms(True)
     kern_warm = kernel_ms(False)
     kern_cold_pair = kernel_ms(True, per_launch=True)
+    # the other arithmetic mode of the same shape on the same box, when it has its own kernel
+    # (the lane kernel's QPGPU_FLAG_FAST build, n <= 8, m <= 16): kernel time and its agreement
+    # with this line's solve of set 0 (status identical; x, f relative error)
+    other = None
+    kname_other = qpgpu.kernel_name(n, p, m, fast=not args.fast)
+    if world == 1 and not args.family and kname_other != kname:
+        launcher(0, 0, cs, not args.fast)()  # first launch of that kernel (code-object load)
+        torch.cuda.synchronize(dev)
+        ko = kernel_ms(True, fast=not args.fast)
+        launcher(0, 0, cs)()
+        torch.cuda.synchronize(dev)
+        ref = [t.clone() for t in outs[0]]
+        launcher(0, 0, cs, not args.fast)()
+        torch.cuda.synchronize(dev)
+        xo, fo, so = outs[0]
+
+        def rel(a_, b_):
+            return float(((a_ - b_).abs() / b_.abs().clamp(min=1.0)).max())
+        ok_ = ref[2] == qpgpu.QP_OK
+        other = {"arithmetic": "exact" if args.fast else "fast", "kernel": kname_other,
+                 "kernel_ms": ko, "frac": bpq * B / (ko * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                 "status_identical": bool(torch.equal(so, ref[2])),
+                 "max_rel_x": rel(xo.reshape(B, -1)[ok_], ref[0].reshape(B, -1)[ok_]) if args.layout == "qp_major" else None,
+                 "max_rel_f": rel(fo[ok_], ref[1][ok_])}
 
     gather_ms = gat.time_one() if gat else None  # one step's gather alone, same payload
 
@@ -497,6 +529,8 @@ def main():
         "status_ok_frac": st_ok,
         "outputs_consistent": consistent,
     }
+    if other:
+        out["other_arithmetic"] = other
     if gather:
         out["gather_ms"] = gather_ms
         out["gather_bytes_per_rank"] = gat.bytes_per_rank

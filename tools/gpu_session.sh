@@ -57,7 +57,7 @@ for s in $STEPS; do
     pmc)
       run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --streams 1
       run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --streams 1
-      python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" C1 65536 "$(python3 -c 'import sys; sys.path.insert(0,"motion-generation-using-quadratic-programs_amd"); import qpgpu; print(qpgpu.kernel_name(7,6,14))')" "$OUT/pmc_traffic.json" ;;
+      python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" C1 65536 "$(python3 -c 'import sys; sys.path.insert(0,"motion-generation-using-quadratic-programs_amd"); import qpgpu; print(qpgpu.kernel_name(7,6,14,fast=True))')" "$OUT/pmc_traffic.json" ;;
     stamps) for l in qp_major tiled64; do run stamps_general_$l 300 python tools/stamps.py general $l; run stamps_box_$l 300 python tools/stamps.py box $l; done ;;
     dist2) run dist2 600 python bench.py --gpus 2 --steps 10 --warmup 2 ;;
     dist2c1) run dist2c1 600 python bench.py --gpus 2 --config C1 --steps 10 --warmup 2 ;;
@@ -78,7 +78,7 @@ for s in $STEPS; do
       run stamps_fast 300 python tools/stamps.py general qp_major fast
       run stamps_exact 300 python tools/stamps.py general qp_major
       for c in ${CONFIGS:-C1 C2}; do
-        run bench_${c}_exact 600 python bench.py --config $c --no-cpu --steps ${ABSTEPS:-30}
+        run bench_${c}_exact 600 python bench.py --config $c --no-cpu --exact --steps ${ABSTEPS:-30}
         run bench_${c}_fast 600 python bench.py --config $c --no-cpu --fast --steps ${ABSTEPS:-30}
       done ;;
     latency)
@@ -138,7 +138,7 @@ PY
         case $c in C5) xa="--steps 2 --warmup 1 --kernel-reps 1";; C3) xa="--steps 3 --warmup 1 --kernel-reps 2";; *) xa="--steps 5 --warmup 1 --kernel-reps 3";; esac
         run pmc_fetch_$c 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$c" -o k -- python3 bench.py --config $c --no-cpu --streams 1 $xa
         run pmc_write_$c 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$c" -o k -- python3 bench.py --config $c --no-cpu --streams 1 $xa
-        read B K < <(python3 -c "import sys; sys.path.insert(0, 'motion-generation-using-quadratic-programs_amd'); import bench, qpgpu; c = bench.CONFIGS['$c']; print(c[4], qpgpu.kernel_name(c[1], c[2], c[3]))")
+        read B K < <(python3 -c "import sys; sys.path.insert(0, 'motion-generation-using-quadratic-programs_amd'); import bench, qpgpu; c = bench.CONFIGS['$c']; print(c[4], qpgpu.kernel_name(c[1], c[2], c[3], fast=True))")
         python3 tools/pmc_traffic.py "$OUT/pmc_fetch_$c" "$OUT/pmc_write_$c" $c $B "$K" "$OUT/pmc_traffic.json"
       done ;;
     listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;

@@ -23,11 +23,14 @@ import sys
 from collections import defaultdict
 
 
-def per_kernel(d, counter):
+def per_kernel(d, counter, fast):
+    # bench.py also times the other arithmetic build of the lane kernel (other_arithmetic): only
+    # the kernels of the measured build count
     vals = defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] == counter and "qp_" in r["Kernel_Name"]:
+            kn = r["Kernel_Name"]
+            if r["Counter_Name"] == counter and "qp_" in kn and ("_fast_" in kn) == fast:
                 vals[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
     return vals
 
@@ -43,8 +46,9 @@ def main():
     lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                        "motion-generation-using-quadratic-programs_amd", "lib", "libqpgpu.so")
     md5 = hashlib.md5(open(lib, "rb").read()).hexdigest() if os.path.exists(lib) else None
-    fe = per_kernel(fetch_dir, "FETCH_SIZE")
-    wr = per_kernel(write_dir, "WRITE_SIZE")
+    fast = "fast" in kname
+    fe = per_kernel(fetch_dir, "FETCH_SIZE", fast)
+    wr = per_kernel(write_dir, "WRITE_SIZE", fast)
     kernels = {}
     for k in sorted(set(fe) | set(wr)):
         fk = statistics.median(fe[k]) if fe[k] else 0.0
