@@ -8,10 +8,12 @@ Workloads (--config; default C1 at N = 1 — the metric config — and C4 at N >
   C1   65 536 x (n=7, p=6, m=14) per GPU (weak scaling)
   C4   1 048 576 x (7, 6, 14) GLOBAL, split into N contiguous shards (131 072 per GPU at N = 8)
   C2, C3, mgqp, C5: the other BASELINE shapes on one GPU (parity-test configs, extra lines).
-With N > 1 each rank solves its own shard (the QPs are independent) and every
-step's results (x, f, status: 68 B per QP at n = 7) are gathered to rank 0 with ONE RCCL gather
-issued on a communication stream, overlapped with the following steps' solves (--no-gather
-turns it off).  `gather_ms` reports one step's gather alone, timed after the run.
+With N > 1 each rank solves its own shard (the QPs are independent) and the
+job's results are collected with ONE RCCL gather to rank 0 (x, f, status of the last step: 68 B
+per QP at n = 7) inside the timed region (--gather final, the default).  The line also carries
+the same steps with a gather per step, overlapped with the following solves on a communication
+stream (`value_gather_every_step`: bound by rank 0's xGMI ingress at N = 8) and with
+none (`value_solve_only`); `gather_ms` is one gather alone, timed after the run.
 
 Cold inputs: a step reads its whole batch from HBM.  The rank keeps R >= 3 distinct resident
 input sets whose total exceeds twice the 256 MiB Infinity Cache when one set is smaller than it
@@ -82,8 +84,11 @@ def parse(argv=None):
                     help="force a kernel family (default: the dispatcher's choice)")
     ap.add_argument("--layout", default="qp_major", choices=["qp_major", "tiled64"],
                     help="batch layout of the resident inputs (include/qpgpu.h)")
-    ap.add_argument("--no-gather", action="store_true",
-                    help="N > 1: skip the per-step RCCL gather of (x, f, status) to rank 0")
+    ap.add_argument("--gather", default="final", choices=["final", "every", "none"],
+                    help="N > 1: the RCCL gather of (x, f, status) to rank 0 — once for the job "
+                         "(the last step's results, inside the timed region; SURVEY.md §8(e)), "
+                         "once per step (overlapped with the next solves), or not at all")
+    ap.add_argument("--no-gather", action="store_true", help="= --gather none")
     ap.add_argument("--streams", type=int, default=3,
                     help="HIP streams the steps are pipelined over (1 = serialized launches)")
     ap.add_argument("--input-sets", type=int, default=0,
@@ -102,6 +107,8 @@ def parse(argv=None):
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--ops-json", default=os.path.join(ROOT, "profiles", "op_counts.json"))
     args = ap.parse_args(argv)
+    if args.no_gather:
+        args.gather = "none"
     if args.exact and args.fast:
         ap.error("--exact and --fast exclude each other")
     args.fast = not args.exact
@@ -294,11 +301,11 @@ def main():
             launchers[key] = v.launcher(stream, family=args.family, fast=fast)
         return launchers[key]
 
-    gather = world > 1 and not args.no_gather
+    gather = world > 1 and args.gather != "none"
     gat = (qpdist.ResultGather(dist, rank, world, S, base.x.shape[0], n, dev, backend)
            if gather else None)
 
-    def step(k, S_=S, use_gather=True):
+    def step(k, S_=S, use_gather=False):
         j = k % S_
         cs = streams[j]
         g = gat if use_gather else None
@@ -316,17 +323,24 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    def timed(K, W, S_, use_gather=True):
+    def timed(K, W, S_, mode="none"):
+        # mode: "final" = the job's one gather (the last step's results to rank 0) after its K
+        # steps, inside the timed region; "every" = one gather per step, overlapped with the
+        # following steps' solves; "none" = the solver alone
         for k in range(W):
-            step(k, S_, use_gather)
+            step(k, S_, mode == "every")
         sync_all()
         t0 = time.perf_counter()
         for k in range(K):
-            step(W + k, S_, use_gather)
+            step(W + k, S_, mode == "every")
+        if mode == "final" and gat:
+            jl = (W + K - 1) % S_
+            gat.wait(jl, streams[jl])
+            gat.submit(jl, *outs[jl], stream=streams[jl])
         sync_all()
         return time.perf_counter() - t0
 
-    elapsed = timed(args.steps, args.warmup, S)
+    elapsed = timed(args.steps, args.warmup, S, args.gather if gat else "none")
     # the last step of every stream slot, checked against set 0's solve rotated (guards the
     # pipelining and the rotated sets): x, f, status bit for bit
     last = {}
@@ -356,9 +370,11 @@ def main():
 
     # the same K steps on one stream (serialized launches)
     elapsed1 = timed(args.steps, 0, 1) if S > 1 else elapsed
-    # N > 1: the same K steps without the per-step gather (the solver alone), so the driver's
-    # scaling curve can separate solver scaling from rank 0's ingress
-    elapsed_solve = timed(args.steps, 0, S, use_gather=False) if gat else None
+    # N > 1: the same K steps without any gather (the solver alone) and with a gather per step
+    # (rank 0 collecting every batch's results), so the driver's scaling curve can separate
+    # solver scaling from rank 0's xGMI ingress
+    elapsed_solve = timed(args.steps, 0, S, "none") if gat else None
+    elapsed_every = (timed(args.steps, 0, S, "every") if args.gather == "final" else elapsed) if gat else None
 
     # kernel-only duration for the roofline: serialized launches on one stream, HIP events on
     # that stream around each launch, rotating over the cold sets (and once more warm)
@@ -436,13 +452,15 @@ def main():
 
     if dist:
         t = torch.tensor([elapsed, elapsed1, kern_cold, kern_warm, gather_ms or 0.0, kern_cold_pair,
-                          elapsed_solve or 0.0],
+                          elapsed_solve or 0.0, elapsed_every or 0.0],
                          dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, elapsed1, kern_cold, kern_warm = (float(v) for v in t[:4])
         kern_cold_pair = float(t[5])
         if elapsed_solve is not None:
             elapsed_solve = float(t[6])
+        if elapsed_every is not None:
+            elapsed_every = float(t[7])
         if gather:
             gather_ms = float(t[4])
         ok_t = torch.tensor([1 if consistent else 0], device=dev if backend == "nccl" else "cpu")
@@ -502,8 +520,9 @@ def main():
     roofline["compute"] = compute
     par = f"batch-sharded x{world}"
     if world > 1:
-        par += (f", {'RCCL' if backend == 'nccl' else backend} gather of (x, f, status) to rank 0 "
-                "per step (overlapped)" if gather else ", no collective")
+        par += ((f", {'RCCL' if backend == 'nccl' else backend} gather of (x, f, status) to rank 0 "
+                 + ("once per job (the last step's results)" if args.gather == "final"
+                    else "per step (overlapped)")) if gather else ", no collective")
     out = {
         "metric": metric_name(cfg, n, p, m, B, world),
         "value": total / elapsed,
@@ -537,8 +556,11 @@ def main():
         out["gather_bytes_per_step_into_rank0"] = gat.bytes_per_rank * (world - 1)
         out["gather_ingress_gbs"] = gat.bytes_per_rank * (world - 1) / (gather_ms * 1e-3) / 1e9
         out["gather_verified"] = gather_ok
+        out["gather_mode"] = args.gather
         out["value_solve_only"] = total / elapsed_solve
         out["ms_per_step_solve_only"] = elapsed_solve * 1e3 / args.steps
+        out["value_gather_every_step"] = total / elapsed_every
+        out["ms_per_step_gather_every_step"] = elapsed_every * 1e3 / args.steps
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(pr, args.cpu_seconds, gpu_sample)
     print(json.dumps(out), flush=True)
