@@ -126,5 +126,10 @@ def test_bench_c4_split_and_cold_sets():
     assert bench.input_set_count(a, (bench.C4_GLOBAL // 2) * c1 // 65536) == 1
     assert bench.input_set_count(bench.parse(["--input-sets", "1"]), c1) == 1
     assert bench.metric_name("C1", 7, 6, 14, 65536, 1).startswith("QP solves/sec at n=7,p=6,m=14 batch=65536")
+    # the job's one gather by default; the fast lane build by default, --exact for the bitwise one
+    assert a.gather == "final" and a.fast and not a.exact
+    assert bench.parse(["--no-gather"]).gather == "none"
+    assert bench.parse(["--gather", "every"]).gather == "every"
+    assert not bench.parse(["--exact"]).fast
     assert "n=30" in bench.metric_name("C3", 30, 6, 60, 65536, 1)
     assert "global batch=1048576 over 8" in bench.metric_name("C4", 7, 6, 14, 131072, 8)
