@@ -18,11 +18,15 @@ print-sched:
 	@echo $(SCHED_$(SRCNAME))
 MK
 )
-for f in qp_layout qp_lane qp_small qp_wave qp_panel qpgpu_api; do [ "$f" = "$SRC" ] || cp "$PKG/lib/$f.o" "$OUT/"; done
+# SCHED_OVERRIDE replaces them ("" = LLVM's default scheduler)
+SCHED=${SCHED_OVERRIDE-$SCHED}
+# the fast lane build is the same source with QPGPU_LANE_FAST (qp_lane_fast.hip) and contraction
+XF=""; [ "$SRC" = qp_lane_fast ] && XF="-ffp-contract=fast"
+for f in qp_layout qp_lane qp_lane_fast qp_small qp_wave qp_panel qpgpu_api; do [ "$f" = "$SRC" ] || cp "$PKG/lib/$f.o" "$OUT/"; done
 (cd "$OUT/tmp" && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-fast-math -fPIC \
-   -std=c++17 -I"$ROOT/include" -I"$PKG/csrc" $SCHED "$@" -c "${SRCFILE:-$PKG/csrc/$SRC.hip}" -o "$OUT/$SRC.o" -save-temps 2>&1 | grep -v warning | grep -v "warnings\? generated" || true)
+   -std=c++17 -I"$ROOT/include" -I"$PKG/csrc" $SCHED $XF "$@" -c "${SRCFILE:-$PKG/csrc/$SRC.hip}" -o "$OUT/$SRC.o" -save-temps 2>&1 | grep -v warning | grep -v "warnings\? generated" || true)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libqpgpu.so" "$OUT"/*.o
-if [ "$SRC" = qp_lane ]; then PAT=qp_lane_kernelILi7ELi14ELi1ELb1ELi6; else PAT=${SRC}_kernel; fi
+if [ "$SRC" = qp_lane ]; then PAT=qp_lane_kernelILi7ELi14ELi1ELb1ELi6; elif [ "$SRC" = qp_lane_fast ]; then PAT=qp_lane_fast_kernelILi7ELi14ELi1ELb1ELi6; else PAT=${SRC}_kernel; fi
 python3 "$ROOT/tools/kernel_regs.py" "$OUT/tmp/$SRC-hip-amdgcn-amd-amdhsa-gfx950.s" "$PAT" > "$OUT/regs.txt"
 rm -rf "$OUT/tmp"
 cat "$OUT/regs.txt"
