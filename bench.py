@@ -51,6 +51,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFS = 78.6  # MI355X FP64 (vector and matrix) peak, AMD spec; no sparsity in FP64
 MALL_BYTES = 256 << 20  # Infinity Cache
 C4_GLOBAL = 1 << 20
+CPU_THREAD_CAP = 16  # a one-GPU job's CPU share on the box (os.cpu_count() is the whole machine)
 # name: (kind, n, p, m, default batch per GPU (0 = C4 split), description)
 CONFIGS = {
     "C1": ("general", 7, 6, 14, 65536, "C1: 65536 x (n=7, p=6, m=14) general QPs per GPU"),
@@ -60,6 +61,16 @@ CONFIGS = {
     "mgqp": ("general", 14, 10, 28, 65536, "mgqp level-0 shape: 65536 x (n=14, p=10, m=28) per GPU"),
     "C5": ("general", 256, 0, 512, 4096, "C5: 4096 x (n=256, p=0, m=512) general QPs per GPU"),
 }
+
+
+def arithmetic_of(kname):
+    """The arithmetic contract of the kernel that actually ran (qpgpu_kernel_name_flags)."""
+    if "fast" in kname:
+        return "fast: fused multiply-adds, shared reciprocals; x, f within 1e-10 relative"
+    if "qp_panel" in kname:
+        return ("tolerance: MFMA panel setup + tree-summed loop sums (n > 64 default); x, f within "
+                "1e-10 relative")
+    return "exact: the reference's operation order, bitwise"
 
 
 def metric_name(cfg, n, p, m, B, world):
@@ -104,6 +115,7 @@ def parse(argv=None):
                          "within north_star's 1e-10 of the reference with the same decisions")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-c4", action="store_true", help="skip the N = 1 line's C4-on-one-GPU record")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--ops-json", default=os.path.join(ROOT, "profiles", "op_counts.json"))
     args = ap.parse_args(argv)
@@ -160,13 +172,19 @@ def cpu_baseline(pr, seconds, gpu_out=None):
         if parity is None and gpu_out is not None:
             xg, fg, sg = (a[:chunk] for a in gpu_out)
             ok = so == 0
-            def rel(a, b):
+            def absrel(a, b):
                 d = np.abs(a - b) / np.maximum(1.0, np.abs(b))
                 return float(d.max()) if d.size else 0.0
+            # north_star's criterion, per QP: ||x - x_ref||_inf / ||x_ref||_inf, |f - f_ref| / |f_ref|
+            exq, efq = qpgpu.rel_error_per_qp(xg[ok], xo[ok], fg[ok], fo[ok])
             parity = {"qps": int(chunk), "status_equal": int((sg == so).sum()),
                       "x_bitwise_equal": bool(np.array_equal(xg[ok].view(np.uint64), xo[ok].view(np.uint64))),
                       "f_bitwise_equal": bool(np.array_equal(fg[ok].view(np.uint64), fo[ok].view(np.uint64))),
-                      "max_rel_err_x": rel(xg[ok], xo[ok]), "max_rel_err_f": rel(fg[ok], fo[ok]),
+                      "max_rel_err_x": float(exq.max()) if exq.size else 0.0,
+                      "max_rel_err_f": float(efq.max()) if efq.size else 0.0,
+                      "rel_err_definition": "per QP: ||x-x_ref||_inf/||x_ref||_inf and |f-f_ref|/|f_ref|",
+                      "max_abs_or_rel_err_x": absrel(xg[ok], xo[ok]),
+                      "max_abs_or_rel_err_f": absrel(fg[ok], fo[ok]),
                       "tolerance": 1e-10, "checker": "oracle/qp_oracle.c on the same QPs"}
         if el >= seconds:
             break
@@ -174,8 +192,9 @@ def cpu_baseline(pr, seconds, gpu_out=None):
            "sample": f"oracle/qp_oracle.c (-O2, 1 thread) re-solving the first {chunk} QPs of the "
                      f"same synthetic batch {done // chunk}x ({done} solves, {el:.1f} s)"}
     # the same restatement on the host's cores, one std::thread per core
-    # over contiguous shards — capped at the CPU share a one-GPU box grants this job (16)
-    threads = max(1, min(16, os.cpu_count() or 1))
+    # over contiguous shards — capped at the CPU share a one-GPU box grants this job (16 threads;
+    # os.cpu_count() reports the whole machine, which this job may not use)
+    threads = max(1, min(CPU_THREAD_CAP, os.cpu_count() or 1))
     big = pr.slice(0, min(pr.batch, chunk * threads * 4))
     done_mt = 0
     t0 = time.perf_counter()
@@ -191,7 +210,9 @@ def cpu_baseline(pr, seconds, gpu_out=None):
             model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
     except OSError:
         pass
-    out["multi_thread"] = {"value": done_mt / el_mt, "threads": threads, "cpu_model": model,
+    out["multi_thread"] = {"value": done_mt / el_mt, "threads": threads, "nproc": os.cpu_count(),
+                           "thread_cap": f"{CPU_THREAD_CAP} = the CPU share of a one-GPU job on the box; "
+                                         f"nproc counts the whole machine", "cpu_model": model,
                            "sample": f"{big.batch} QPs per pass, {done_mt // big.batch} passes, "
                                      f"{el_mt:.1f} s"}
     out["cpu_model"] = model
@@ -355,12 +376,11 @@ def main():
 
     # (TILED64: the shifts are whole 64-QP tiles, so the same flat roll un-rotates x, f, status)
     consistent = True
-    if True:
-        for j, r in last.items():
-            x_, f_, s_ = outs[j]
-            consistent &= bool(torch.equal(unrot(x_, r, n), unrot(ref_x, ref_r, n))
-                               and torch.equal(unrot(f_, r, 1), unrot(ref_f, ref_r, 1))
-                               and torch.equal(unrot(s_, r, 1), unrot(ref_s, ref_r, 1)))
+    for j, r in last.items():
+        x_, f_, s_ = outs[j]
+        consistent &= bool(torch.equal(unrot(x_, r, n), unrot(ref_x, ref_r, n))
+                           and torch.equal(unrot(f_, r, 1), unrot(ref_f, ref_r, 1))
+                           and torch.equal(unrot(s_, r, 1), unrot(ref_s, ref_r, 1)))
     st_ok = float((unrot(ref_s, ref_r, 1) == qpgpu.QP_OK).float().mean())
     gather_ok = None
     if gat and rank == 0:
@@ -416,21 +436,68 @@ def main():
         ko = kernel_ms(True, fast=not args.fast)
         launcher(0, 0, cs)()
         torch.cuda.synchronize(dev)
-        ref = [t.clone() for t in outs[0]]
+        mine = [t.clone() for t in outs[0]]
         launcher(0, 0, cs, not args.fast)()
         torch.cuda.synchronize(dev)
-        xo, fo, so = outs[0]
-
-        def rel(a_, b_):
-            return float(((a_ - b_).abs() / b_.abs().clamp(min=1.0)).max())
-        ok_ = ref[2] == qpgpu.QP_OK
-        other = {"arithmetic": "exact" if args.fast else "fast", "kernel": kname_other,
+        theirs = [t.clone() for t in outs[0]]
+        # the exact (bitwise) build's output is the reference of the comparison, whichever
+        # build this line measures
+        ex_, fa_ = (theirs, mine) if args.fast else (mine, theirs)
+        ok_ = (ex_[2] == qpgpu.QP_OK).cpu().numpy()
+        if args.layout == "qp_major":
+            exq, efq = qpgpu.rel_error_per_qp(fa_[0].reshape(B, -1).cpu().numpy()[ok_],
+                                              ex_[0].reshape(B, -1).cpu().numpy()[ok_],
+                                              fa_[1].cpu().numpy()[ok_], ex_[1].cpu().numpy()[ok_])
+        else:
+            exq, efq = None, qpgpu.rel_error_per_qp(np.zeros((int(ok_.sum()), 0)), np.zeros((int(ok_.sum()), 0)),
+                                                    fa_[1].cpu().numpy()[ok_], ex_[1].cpu().numpy()[ok_])[1]
+        other = {"arithmetic": arithmetic_of(kname_other), "kernel": kname_other,
                  "kernel_ms": ko, "frac": bpq * B / (ko * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                 "status_identical": bool(torch.equal(so, ref[2])),
-                 "max_rel_x": rel(xo.reshape(B, -1)[ok_], ref[0].reshape(B, -1)[ok_]) if args.layout == "qp_major" else None,
-                 "max_rel_f": rel(fo[ok_], ref[1][ok_])}
+                 "status_identical": bool(torch.equal(mine[2], theirs[2])),
+                 "max_rel_x": (float(exq.max()) if exq is not None and exq.size else None),
+                 "max_rel_f": float(efq.max()) if efq.size else 0.0,
+                 "rel_err_of": "the fast build against the exact build, per QP (||dx||_inf/||x||_inf, |df|/|f|)"}
 
     gather_ms = gat.time_one() if gat else None  # one step's gather alone, same payload
+
+    # The N = 1 line's denominator for the driver's N > 1 lines (which run C4: 1 048 576 QPs
+    # split over the ranks, strong scaling): the same C4 global batch solved on this one GPU,
+    # timed the same way (K steps pipelined over S streams, synchronized on both sides).
+    c4_one = None
+    if world == 1 and cfg == "C1" and not args.batch and not args.no_c4:
+        prc4 = qpgpu.make_problems("general", 7, 6, 14, 0, C4_GLOBAL, seed=args.seed)
+        b4 = qpgpu.DeviceBatch(prc4, dev, with_iters=False, layout=args.layout)
+        del prc4
+        outs4 = [(torch.empty_like(b4.x), torch.empty_like(b4.f), torch.empty_like(b4.status))
+                 for _ in range(S)]
+        l4 = []
+        for j in range(S):
+            v = b4.__class__.__new__(b4.__class__)
+            v.__dict__.update(b4.__dict__)
+            v.x, v.f, v.status = outs4[j]
+            l4.append(v.launcher(streams[j], fast=args.fast))
+        for k in range(args.warmup):
+            l4[k % S]()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            l4[k % S]()
+        torch.cuda.synchronize(dev)
+        el4 = time.perf_counter() - t0
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(streams[0])
+        for _ in range(args.kernel_reps):
+            l4[0]()
+        e1.record(streams[0])
+        torch.cuda.synchronize(dev)
+        k4 = e0.elapsed_time(e1) / args.kernel_reps
+        c4_one = {"batch": C4_GLOBAL, "value": C4_GLOBAL * args.steps / el4,
+                  "ms_per_step": el4 * 1e3 / args.steps, "streams": S, "kernel_ms": k4,
+                  "hbm_frac": bpq * C4_GLOBAL / (k4 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                  "note": "C4's global batch on this one GPU (cold: 1.9 GB of inputs > Infinity "
+                          "Cache), the same timing as `value`: the denominator of the N > 1 C4 lines"}
+        del b4, outs4, l4
+        torch.cuda.empty_cache()
 
     # l1-pass histogram of one resident set (SURVEY.md §5 metrics): one more solve with the
     # per-QP pass counts on
@@ -509,7 +576,7 @@ def main():
     compute = None
     if flops_rec:
         tf = flops_rec["flops"] / (kern_cold * 1e-3) / 1e12
-        compute = {"bound": "mfma", "achieved": tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+        compute = {"bound": "fp64", "achieved": tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                    "frac": tf / FP64_PEAK_TFS, "flops_per_launch": flops_rec["flops"],
                    "flops_per_qp": flops_rec["per_qp"], "div_per_qp": flops_rec.get("div_per_qp"),
                    "sqrt_per_qp": flops_rec.get("sqrt_per_qp"), "flops_source": flops_rec.get("source")}
@@ -518,6 +585,13 @@ def main():
     roofline = dict(primary)
     roofline["hbm"] = hbm
     roofline["compute"] = compute
+    # the whole-job rate in the same terms: algorithmic bytes per step / ms_per_step.  With S > 1
+    # streams consecutive steps overlap (different batches' kernels co-resident on the CUs), so
+    # this can exceed the per-launch figure above; with S = 1 they agree up to launch gaps.
+    pipe_gbs = bpq * B / (elapsed / args.steps) / 1e9
+    roofline["pipelined"] = {"achieved": pipe_gbs, "frac": pipe_gbs / HBM_PEAK_GBS, "unit": "GB/s",
+                             "streams": S, "ms_per_step": elapsed * 1e3 / args.steps,
+                             "per_launch_frac": hbm["frac"]}
     par = f"batch-sharded x{world}"
     if world > 1:
         par += ((f", {'RCCL' if backend == 'nccl' else backend} gather of (x, f, status) to rank 0 "
@@ -538,10 +612,10 @@ def main():
         "data": "synthetic",
         "config": {"workload": desc, "kind": kind, "n": n, "p": p, "m": m, "batch_per_gpu": B,
                    "global_batch": B * world, "kernel": kname, "layout": args.layout,
-                   "arithmetic": ("fast: fused multiply-adds, shared reciprocals; x, f within 1e-10"
-                                  if args.fast else "exact: the reference's operation order, bitwise"),
+                   "arithmetic": arithmetic_of(kname),
                    "streams": S, "input_sets": R, "cold_inputs": R > 1 or in_bytes * B >= 2 * MALL_BYTES,
                    "backend": backend if world > 1 else None, "parallelism": par},
+        "per_gpu_batch": B,
         "value_streams1": total / elapsed1,
         "roofline": roofline,
         "l1_pass_histogram": hist,
@@ -561,6 +635,8 @@ def main():
         out["ms_per_step_solve_only"] = elapsed_solve * 1e3 / args.steps
         out["value_gather_every_step"] = total / elapsed_every
         out["ms_per_step_gather_every_step"] = elapsed_every * 1e3 / args.steps
+    if c4_one:
+        out["c4_one_gpu"] = c4_one
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(pr, args.cpu_seconds, gpu_sample)
     print(json.dumps(out), flush=True)

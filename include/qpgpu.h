@@ -99,16 +99,18 @@ enum qpgpu_error {
                                           and iteration counts) instead.  Implied by
                                           QPGPU_FLAG_WRITE_FACTOR. */
 
-#define QPGPU_FLAG_FAST 0x4u          /* shapes the lane kernel serves (n <= 8, m <= 16): run its
-                                          fast build — multiply-adds fused, one refined
-                                          reciprocal per shared divisor, rotation lengths as
+#define QPGPU_FLAG_FAST 0x4u          /* n <= 64, m <= 256 (the lane kernel's shapes and the wave
+                                          kernel's LDS variants: C1, C2, the mgqp levels, C3):
+                                          run the fast builds — multiply-adds fused, one refined
+                                          reciprocal per divisor, rotation lengths as
                                           sqrt(a^2 + b^2) inside the exponent range — whose x and
-                                          f match the reference within 1e-10 relative
-                                          (|a - b| / max(1, |b|)) with the same decisions on
-                                          well-conditioned problems, instead of bit for bit.
-                                          Other shapes run as without it.  Not combinable with
-                                          QPGPU_FLAG_EXACT or QPGPU_FLAG_WRITE_FACTOR
-                                          (QPGPU_ERR_INVALID_ARGUMENT). */
+                                          f match the reference within 1e-10 relative per QP
+                                          (||x - x_ref||_inf / ||x_ref||_inf, |f - f_ref| /
+                                          |f_ref|) with the same decisions on well-conditioned
+                                          problems, instead of bit for bit.  Other shapes run as
+                                          without it (n > 64 already defaults to the 1e-10 MFMA
+                                          panel path).  Not combinable with QPGPU_FLAG_EXACT or
+                                          QPGPU_FLAG_WRITE_FACTOR (QPGPU_ERR_INVALID_ARGUMENT). */
 
 /* Kernel-family selection (benchmarking / testing knobs; default = fastest for the shape):
  *   LANE      one QP per lane (qp_lane.hip, n <= 8, m <= 16)
@@ -116,10 +118,16 @@ enum qpgpu_error {
  *   WAVE      one QP per 32/64/256 lanes, LDS / workspace state (qp_wave.hip, n <= 256,
  *             m <= 1024; n > 64 uses a cached device workspace of ~1 MiB per QP, allocated by
  *             the first call for that size — call once before capturing into a hipGraph)
+ *   GENERIC   one QP per 256-thread workgroup, every array in a device workspace sized from
+ *             (n, m) at run time (qp_generic.hip): ANY shape with n*n and n*m below 2^31, as the
+ *             reference's solve_quadprog takes any n, p, m (QuadProg++.hh:69-72).  The default
+ *             for the shapes no other family covers (n > 256 or m > 1024); bitwise with the
+ *             reference's operation order; ~2 n^2 + 12 n + 2 m doubles of workspace per QP.
  * Forcing a family that does not cover the shape returns QPGPU_ERR_UNSUPPORTED_SHAPE. */
 #define QPGPU_FLAG_FORCE_LANE 0x100u
 #define QPGPU_FLAG_FORCE_SUBGROUP 0x200u
 #define QPGPU_FLAG_FORCE_WAVE 0x400u
+#define QPGPU_FLAG_FORCE_GENERIC 0x800u
 
 typedef struct qpgpu_problem_desc {
   int32_t n;         /* variables                      (G.ncols() in the reference)  */
@@ -178,14 +186,17 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d,
 int qpgpu_relayout(int64_t batch, int32_t elems, const double* src, double* dst, int32_t to_tiled,
                    void* stream);
 
-/* Largest n / m / p the compiled kernels accept (0 if no device code). */
+/* Largest n / m the specialised kernels accept (lane / subgroup / wave families); larger shapes
+ * run on the generic kernel (QPGPU_FLAG_FORCE_GENERIC), whose only limits are n*n < 2^31 and
+ * n*m < 2^31 and device memory for its workspace. */
 int qpgpu_max_n(void);
 int qpgpu_max_m(void);
 
 /* Name of the kernel variant qpgpu_solve_batched would launch for this shape ("" if none). */
 const char* qpgpu_kernel_name(int32_t n, int32_t p, int32_t m);
 /* The same for a launch with these QPGPU_FLAG_* flags (QPGPU_FLAG_FAST selects the lane
- * kernel's fast build where it covers the shape). */
+ * kernel's fast build where it covers the shape); "" for a flag combination the solve entry
+ * points reject (unknown bits, FAST with EXACT or WRITE_FACTOR, two forced families). */
 const char* qpgpu_kernel_name_flags(int32_t n, int32_t p, int32_t m, uint32_t flags);
 
 /* Human-readable text for the last QPGPU_ERR_HIP on this thread. */

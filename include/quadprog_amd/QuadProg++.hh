@@ -12,11 +12,13 @@
 // Implemented by libquadprog_amd.so on top of the gfx950 kernels (include/qpgpu.h); every
 // call runs on the GPU.
 //
-// Differences from the reference's contract (QuadProg++ solves any size and has no GPU):
-//   * size limits: the compiled kernels cover 1 <= n <= 256 and m <= 1024 (p <= n in practice;
-//     qpgpu_max_n() / qpgpu_max_m()).  n == 0 throws std::logic_error("qpgpu: n == 0 is not
-//     supported (undefined in QuadProg++)"); a larger shape throws
-//     std::runtime_error("qpgpu: solve failed (code 2): no gfx950 kernel covers this (n, p, m)");
+// Any n, p, m is solved, as by the reference (QuadProg++.hh:69-72): shapes beyond the specialised
+// kernels (n > 256 or m > 1024) run on the generic workspace kernel (qp_generic.hip), bit for bit
+// like the others.  Differences from the reference's contract (it has no GPU):
+//   * n == 0 throws std::logic_error("qpgpu: n == 0 is not supported (undefined in
+//     QuadProg++)"); n*n or n*m at or above 2^31 (an 8 GiB G), beyond the generic kernel's
+//     indexing, throws std::runtime_error("qpgpu: solve failed (code 2): no gfx950 kernel covers
+//     this (n, p, m)");
 //   * no usable GPU: std::runtime_error("qpgpu: solve failed (code 4): ...") (code 3 for another
 //     HIP runtime failure, with its message);
 //   * the safety cap on active-set steps (1000 + 100 (n + p + m)), which terminating problems

@@ -180,11 +180,12 @@ void InputPort<T>::disconnect() {
 // TaskContext::ports(): the component's named ports
 class DataFlowInterface {
  public:
-  base::PortInterface& addPort(base::PortInterface& p) {
-    ports_[p.getName()] = &p;
-    return p;
-  }
+  // As RTT 2.x's DataFlowInterface::addLocalPort: a port added under a name that is already
+  // present replaces it, and the replaced port is first removed, which disconnects it
+  // (removeLocalPort -> PortInterface::disconnect()), even when it is the same port object.
+  base::PortInterface& addPort(base::PortInterface& p) { return addPort(p.getName(), p); }
   base::PortInterface& addPort(const std::string& name, base::PortInterface& p) {
+    removePort(name);
     ports_[name] = &p;
     return p;
   }

@@ -91,9 +91,10 @@ void MotionGenerationQuadraticProgram::setDOFsize(unsigned int DOFsize) {
   if (portsPrepared_) {
     // The reference removes the 10 limit ports by names without the "_port" suffix
     // (src/mgqp.cpp:187-196) although it registers them with it (:412-469), so those 10 are
-    // never removed: kept as is (DESIGN Appendix A).  Re-adding them below replaces the map
-    // entries with the same member ports, as RTT's addPort does for an existing name, and
-    // their connections survive the second setDOFsize.
+    // not removed here: kept as is (DESIGN Appendix A).  Re-adding them below goes through
+    // RTT's addPort, which removes (and so disconnects) a port already registered under the
+    // same name before adding the new one: the limit ports stay registered but lose their
+    // connections, like every other port.
     for (const char* s : {"in_robotstatus_port", "out_torques_port", "out_jointPosLimitInf",
                           "out_jointPosLimitSup", "out_jointVelLimitInf", "out_jointVelLimitSup",
                           "out_jointAccLimitInf", "out_jointAccLimitSup", "out_jointAccDynLimitInf",

@@ -60,6 +60,144 @@ __device__ __forceinline__ double qp_distance_libm(double a, double b) {
   return (gt || lt) ? h : a1 * kSqrt2;
 }
 
+// Sequential sums over runtime-length index ranges with the operand loads batched kU at a time
+// (qp_wave.hip, qp_generic.hip): all kU loads of a chunk are issued before the chunk's
+// multiply-adds, so a loop over global (or LDS) operands costs one memory latency per chunk
+// instead of one per element.  The adds stay strictly sequential in the reference's index
+// order, so results are bit-identical to the plain loops.
+// s + sum_{j=j0}^{j1-1} A(j) * B(j), j ascending (s += a*b per element).  Full chunks of kU
+// issue all their loads unpredicated before the chunk's multiply-adds; the remainder is one
+// predicated chunk.
+template <int kU, class FA, class FB>
+__device__ __forceinline__ double seq_fma_up(double s, int j0, int j1, FA A, FB B) {
+  if constexpr (kU == 1) {
+    for (int j = j0; j < j1; j++) s += A(j) * B(j);
+    return s;
+  }
+  int jb = j0;
+  for (; jb + kU <= j1; jb += kU) {
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      va[u] = A(jb + u);
+      vb[u] = B(jb + u);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) s += va[u] * vb[u];
+  }
+  if (jb < j1) {  // partial chunk: loads predicated, still one latency
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      va[u] = jb + u < j1 ? A(jb + u) : 0.0;
+      vb[u] = jb + u < j1 ? B(jb + u) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++)
+      if (jb + u < j1) s += va[u] * vb[u];
+  }
+  return s;
+}
+
+// seq_fma_up for operands in LDS with s starting at +0.0: the partial chunk's loads are
+// unconditional (past j1 they read whatever lies there — in-bounds LDS) and its products past
+// j1 are replaced by +0.0, so there is no exec-mask branch per load.  A sum that starts at
+// +0.0 is never -0.0 (a sum is -0.0 only from two -0.0 operands), so adding +0.0 leaves it
+// unchanged.
+template <int kU, class FA, class FB>
+__device__ __forceinline__ double seq_fma_up_lds(double s, int j0, int j1, FA A, FB B) {
+  int jb = j0;
+  for (; jb + kU <= j1; jb += kU) {
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      va[u] = A(jb + u);
+      vb[u] = B(jb + u);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) s += va[u] * vb[u];
+  }
+  if (jb < j1) {
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      va[u] = A(jb + u);
+      vb[u] = B(jb + u);
+    }
+    const int c = j1 - jb;
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const double q = va[u] * vb[u];
+      s += u < c ? q : 0.0;
+    }
+  }
+  return s;
+}
+
+// s - sum A(j) * B(j), j ascending (s -= a*b per element)
+template <int kU, class FA, class FB>
+__device__ __forceinline__ double seq_fms_up(double s, int j0, int j1, FA A, FB B) {
+  if constexpr (kU == 1) {
+    for (int j = j0; j < j1; j++) s -= A(j) * B(j);
+    return s;
+  }
+  int jb = j0;
+  for (; jb + kU <= j1; jb += kU) {
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      va[u] = A(jb + u);
+      vb[u] = B(jb + u);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) s -= va[u] * vb[u];
+  }
+  if (jb < j1) {
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      va[u] = jb + u < j1 ? A(jb + u) : 0.0;
+      vb[u] = jb + u < j1 ? B(jb + u) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++)
+      if (jb + u < j1) s -= va[u] * vb[u];
+  }
+  return s;
+}
+
+// s - sum A(k) * B(k), k DEscending from k1-1 down to k0 (s -= a*b per element)
+template <int kU, class FA, class FB>
+__device__ __forceinline__ double seq_fms_down(double s, int k0, int k1, FA A, FB B) {
+  if constexpr (kU == 1) {
+    for (int k = k1 - 1; k >= k0; k--) s -= A(k) * B(k);
+    return s;
+  }
+  int kb = k1 - 1;
+  for (; kb - kU + 1 >= k0; kb -= kU) {
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      va[u] = A(kb - u);
+      vb[u] = B(kb - u);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) s -= va[u] * vb[u];
+  }
+  if (kb >= k0) {
+    double va[kU], vb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      va[u] = kb - u >= k0 ? A(kb - u) : 0.0;
+      vb[u] = kb - u >= k0 ? B(kb - u) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++)
+      if (kb - u >= k0) s -= va[u] * vb[u];
+  }
+  return s;
+}
+
 // Ordering point for LDS hand-offs between lanes of ONE wavefront.  A QP is always owned by
 // lanes of a single wave that are converged with each other (every control decision is a
 // function of replicated values), and a wave's LDS instructions execute in issue order, so a

@@ -46,9 +46,19 @@
 #define QPK_LANE_C(name) name
 #endif
 
+// Diagnostic s_memtime stamps (tools/stamps.py): compiled in only when QPGPU_LANE_STAMPS is 1
+// (A/B builds); the product build carries none of their SGPR state.
+#ifndef QPGPU_LANE_STAMPS
+#define QPGPU_LANE_STAMPS 1
+#endif
+
 namespace QPK_LANE_NS {
 using namespace qpk;
 constexpr bool kFast = QPGPU_LANE_FAST != 0;
+constexpr bool kStamps = QPGPU_LANE_STAMPS != 0;
+__device__ __forceinline__ void lstamp(const QpArgs& a, int slot) {
+  if constexpr (kStamps) lstamp(a, slot);
+}
 
 template <typename T>
 __device__ __forceinline__ T opq_l(T v) {
@@ -183,8 +193,13 @@ __device__ __forceinline__ double ldistance(double a, double b, bool& ok) {
 // PX >= 0: p is the compile-time constant PX as well (C1/C4: 6, C2: 0), which folds every
 // [p, iq) loop of the active-set phase (for n = 7, p = 6 that range holds at most one entry).
 // The solve of one wave's 64 QPs.  SAFE: the IEEE forms of division and distance (the exact
-// build always; the fast build's fallback).  Returns false, having written nothing, when the
-// fast forms were not valid for some lane (then the caller re-solves with SAFE).
+// build always; the fast build's fallback).  Returns false as soon as a fast form was not
+// valid for some lane (checked after the equality phase and at every loop pass): x, f, status
+// and iters are not written then, and the caller re-solves the wave with SAFE, which rewrites
+// everything — including the m = 0 snapshot (x_eq, f_eq, st_eq) the fast attempt may already
+// have written.  In the fast build (-ffp-contract=fast) the SAFE body's multiply-adds are
+// contracted too: a fallback wave keeps the reference's divisions and distance(), not its
+// bitwise results (still within 1e-10).
 template <int NM, int MM, int T, bool EXACT, int PX, bool SAFE>
 __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
   static_assert(MM <= 64, "bitmask bookkeeping holds m <= 64");
@@ -308,7 +323,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
                                          (__attribute__((address_space(3))) void*)(sbuf + k * 2 * kQpw),
                                          16, 0, 0);
   };
-  qp_stamp(a, 0);
+  lstamp(a, 0);
 
   // ---------------------------------------------------------------- setup
   bool chol_ok = live;  // idle lanes (past the batch) never touch LDS slots
@@ -335,7 +350,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
       g0v[i] = live ? v0 : 0.0;
     }
     __syncthreads();
-    qp_stamp(a, 9);  // diagnostic: G / g0 in registers
+    lstamp(a, 9);  // diagnostic: G / g0 in registers
     // round B: CE and ce0 (equality phase), landing during the Cholesky, the J build and the
     // solve.  A full wave issues its span a part per Cholesky row: issued at once, its LDS-DMA
     // instructions held the wave's issue until most of the data had arrived (the CU's memory
@@ -408,7 +423,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
       const int offc = (kQpw * np_ + 127) / 128 * 128;
       ce_staged = offc + kQpw * p <= STAGE;
       __syncthreads();
-      qp_stamp(a, 10);  // diagnostic: round B (CE) landed
+      lstamp(a, 10);  // diagnostic: round B (CE) landed
       if constexpr (kCiDma && PX > 0) {
         if (dma && ce_staged) {
           // CE / ce0 -> AGPRs, then the LDS is the CI copy's (round C)
@@ -424,7 +439,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
           }
           ce_agpr = true;
           __syncthreads();
-          qp_stamp(a, 11);  // diagnostic: CE in AGPRs
+          lstamp(a, 11);  // diagnostic: CE in AGPRs
           // the rows past the LDS copy (and ci0) warmed here; the copy itself goes a part per
           // equality step.  Measured (profiles/r03_s10): C1 kernel 47.4 us with the warm-up
           // here, 48.6 without it, 49.9 with it at the first equality step
@@ -513,7 +528,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
       warmup();
     }
   }
-  qp_stamp(a, 1);
+  lstamp(a, 1);
   // Without the DMA: touch every cache line of this lane's CI and ci0 blocks before the
   // equality phase: the loads complete during it (nothing waits on them until its end), so the
   // first l1 scan reads L2 / MALL instead of queueing on one chip-wide HBM burst.  Issued after
@@ -870,7 +885,14 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
   }
   // element e (= row * MM + column) of this lane's CI from the LDS copy (e < kCiRows * MM)
   auto ci_lds_at = [&](int e) -> double { return sbuf[((e >> 1) * kQpw + lane) * 2 + (e & 1)]; };
-  qp_stamp(a, 2);
+  lstamp(a, 2);
+  // Fast build: a fast form that went out of range in the setup or the equality phase (or
+  // non-finite data) sends the wave to the IEEE re-solve now, instead of after a loop that
+  // would run on garbage up to the step cap.  (The CE / CI copies into LDS have landed: the
+  // re-solve may restage.)
+  if constexpr (F) {
+    if (wave_any(!fok)) return false;
+  }
 
   // ---------------------------------------------------------------- active-set loop
   // Wave-uniform loop: every lane stays until all 64 are done; per-lane work is predicated on
@@ -1074,10 +1096,13 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
     };
     uint64_t tscan = 0, tsel = 0, nloop = 0, tfirst = 0;  // diagnostic stamps only
     while (wave_any(active)) {
-      const uint64_t tl0 = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+      if constexpr (F) {
+        if (wave_any(!fok)) return false;  // (as above; the loop issues no LDS-DMA)
+      }
+      const uint64_t tl0 = (kStamps && a.stamps) ? __builtin_amdgcn_s_memtime() : 0;
       scan_pass();
-      const uint64_t tl1 = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
-      if (a.stamps) {
+      const uint64_t tl1 = (kStamps && a.stamps) ? __builtin_amdgcn_s_memtime() : 0;
+      if (kStamps && a.stamps) {
         tscan += tl1 - tl0;
         if (nloop == 0) tfirst = tl1 - tl0;
       }
@@ -1103,7 +1128,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
           lput_lo<IQLO>(Av, iq, ip);
         }
       }
-      if (a.stamps) {
+      if (kStamps && a.stamps) {
         // make the select's loads part of the select span
         const double sink = npv[0] + ci0ip;
         asm volatile("" ::"v"(sink));
@@ -1193,14 +1218,14 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
         }
       }
     }
-    if (a.stamps && lane == 0) {
+    if (kStamps && a.stamps && lane == 0) {
       a.stamps[(uint64_t)blockIdx.x * kStampSlots + 5] = tscan;
       a.stamps[(uint64_t)blockIdx.x * kStampSlots + 6] = tsel;
       a.stamps[(uint64_t)blockIdx.x * kStampSlots + 7] = nloop;
       a.stamps[(uint64_t)blockIdx.x * kStampSlots + 8] = tfirst;
     }
   }
-  qp_stamp(a, 3);
+  lstamp(a, 3);
   if constexpr (F) {
     if (wave_any(!fok)) return false;
   }
@@ -1216,7 +1241,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
     a.status[b] = status;
     if (a.iters) a.iters[b] = iter;
   }
-  qp_stamp(a, 4);
+  lstamp(a, 4);
   return true;
 }
 
@@ -1237,6 +1262,13 @@ template <int NM, int MM, int T>
 static void launch_lane_t(const QpArgs& a, hipStream_t stream) {
   const int64_t blocks = (a.batch + kQpw - 1) / kQpw;
   const dim3 g((unsigned)blocks), blk(64);
+#ifdef QPGPU_LANE_AB_C1ONLY
+  // A/B experiment builds (tools/ab_build.sh): only the C1 instantiation, for a quick compile
+  if constexpr (NM == 7 && MM == 14 && T == 1)
+    if (a.n == NM && a.m == MM && !a.x_eq && a.p == 6)
+      hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, 6>), g, blk, 0, stream, a);
+  return;
+#endif
   if (a.n == NM && a.m == MM && !a.x_eq) {
     if (a.p == 6)
       hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, 6>), g, blk, 0, stream, a);

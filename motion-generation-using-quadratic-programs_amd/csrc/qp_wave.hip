@@ -14,6 +14,16 @@
 // State lives in LDS (per QP: J and R [n][n+1], vectors, bookkeeping) with dynamic indexing;
 // with GJR, J and R live in a global workspace instead (n = 256: 2 x 514 KiB per QP).  The
 // lead lane exchanges scalars with its subgroup through an LDS control block.
+//
+// The same source built a second time with QPGPU_WAVE_FAST=1 and -ffp-contract=fast
+// (qp_wave_fast.hip) is the QPGPU_FLAG_FAST kernel for the LDS variants (n <= 64, m <= 256:
+// the mgqp hierarchy levels, C3): the lead's serial chains — add_constraint's |h| chain, the
+// Givens coefficients of add_constraint and delete_constraint, update_r's back-substitution,
+// the step lengths t1 / t2 — and the setup's divisions use one refined reciprocal per divisor
+// and distance() as sqrt(a^2 + b^2) (rsq + refinement), multiply-adds fused.  Same algorithm
+// and decisions; x and f within north_star's 1e-10 relative instead of bit-identical.  Every
+// fast form checks that its operands are well inside the exponent range; a wave with any
+// failed check re-solves with the IEEE forms.
 #include <climits>
 #include <cstdlib>
 
@@ -21,7 +31,72 @@
 
 #include "qp_common.h"
 
-namespace qpk {
+#ifndef QPGPU_WAVE_FAST
+#define QPGPU_WAVE_FAST 0
+#endif
+#if QPGPU_WAVE_FAST
+#define QPK_WAVE_NS qpk_wfast
+#define QP_WAVE_KERNEL qp_wave_fast_kernel
+#else
+#define QPK_WAVE_NS qpk
+#define QP_WAVE_KERNEL qp_wave_kernel
+#endif
+
+namespace QPK_WAVE_NS {
+using namespace qpk;
+constexpr bool kWaveFast = QPGPU_WAVE_FAST != 0;
+
+// ---- the fast build's arithmetic (F = kWaveFast and not the IEEE fallback body)
+// 1 / b: v_rcp_f64 + the two Newton steps of the compiler's own division sequence (without its
+// range scaling and special-case fix-up); valid when the result is a normal number
+__device__ __forceinline__ double wrcp(double b) {
+  double y = __builtin_amdgcn_rcp(b);
+  double e = __builtin_fma(-b, y, 1.0);
+  y = __builtin_fma(y, e, y);
+  e = __builtin_fma(-b, y, 1.0);
+  return __builtin_fma(y, e, y);
+}
+__device__ __forceinline__ bool wrcp_ok(double r) {
+  return __builtin_amdgcn_class(r, 0x108);  // +-normal
+}
+// a / b given rb = wrcp(b) (F); a / b otherwise
+template <bool F>
+__device__ __forceinline__ double wdiv_r(double a, double b, double rb, bool& ok) {
+  if constexpr (F) {
+    ok = ok && wrcp_ok(rb);
+    return a * rb;
+  } else {
+    return a / b;
+  }
+}
+template <bool F>
+__device__ __forceinline__ double wdiv(double a, double b, bool& ok) {
+  if constexpr (F)
+    return wdiv_r<true>(a, b, wrcp(b), ok);
+  else
+    return a / b;
+}
+// distance(a, b) (F): sqrt(a^2 + b^2) by v_rsq_f64 + one Goldschmidt refinement and a final
+// Newton correction, valid for a^2 + b^2 in [2^-600, 2^600] (exactly 0 when a = b = 0, as the
+// reference's); otherwise the reference's scaled form (qp_distance)
+template <bool F>
+__device__ __forceinline__ double wdist(double a, double b, bool& ok) {
+  if constexpr (F) {
+    const double s = __builtin_fma(a, a, b * b);
+    const double y = __builtin_amdgcn_rsq(s);
+    double g = s * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    const double d = __builtin_fma(-g, g, s);
+    g = __builtin_fma(d, h, g);
+    const bool z = (a == 0.0) && (b == 0.0);
+    ok = ok && (z || (s >= 0x1p-600 && s <= 0x1p600));
+    return z ? 0.0 : g;
+  } else {
+    return qp_distance(a, b);
+  }
+}
 
 template <int S>
 __device__ __forceinline__ void grp_sync() {
@@ -49,139 +124,6 @@ __device__ __forceinline__ void grp_sync() {
 #define QPGPU_WAVE_KUDZ 8
 #endif
 constexpr int kUG = 8, kUL = QPGPU_WAVE_KUL;
-
-// s + sum_{j=j0}^{j1-1} A(j) * B(j), j ascending (s += a*b per element).  Full chunks of kU
-// issue all their loads unpredicated before the chunk's multiply-adds; the remainder is one
-// predicated chunk.
-template <int kU, class FA, class FB>
-__device__ __forceinline__ double seq_fma_up(double s, int j0, int j1, FA A, FB B) {
-  if constexpr (kU == 1) {
-    for (int j = j0; j < j1; j++) s += A(j) * B(j);
-    return s;
-  }
-  int jb = j0;
-  for (; jb + kU <= j1; jb += kU) {
-    double va[kU], vb[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      va[u] = A(jb + u);
-      vb[u] = B(jb + u);
-    }
-#pragma unroll
-    for (int u = 0; u < kU; u++) s += va[u] * vb[u];
-  }
-  if (jb < j1) {  // partial chunk: loads predicated, still one latency
-    double va[kU], vb[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      va[u] = jb + u < j1 ? A(jb + u) : 0.0;
-      vb[u] = jb + u < j1 ? B(jb + u) : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; u++)
-      if (jb + u < j1) s += va[u] * vb[u];
-  }
-  return s;
-}
-
-// seq_fma_up for operands in LDS with s starting at +0.0: the partial chunk's loads are
-// unconditional (past j1 they read whatever lies there — in-bounds LDS) and its products past
-// j1 are replaced by +0.0, so there is no exec-mask branch per load.  A sum that starts at
-// +0.0 is never -0.0 (a sum is -0.0 only from two -0.0 operands), so adding +0.0 leaves it
-// unchanged.
-template <int kU, class FA, class FB>
-__device__ __forceinline__ double seq_fma_up_lds(double s, int j0, int j1, FA A, FB B) {
-  int jb = j0;
-  for (; jb + kU <= j1; jb += kU) {
-    double va[kU], vb[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      va[u] = A(jb + u);
-      vb[u] = B(jb + u);
-    }
-#pragma unroll
-    for (int u = 0; u < kU; u++) s += va[u] * vb[u];
-  }
-  if (jb < j1) {
-    double va[kU], vb[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      va[u] = A(jb + u);
-      vb[u] = B(jb + u);
-    }
-    const int c = j1 - jb;
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      const double q = va[u] * vb[u];
-      s += u < c ? q : 0.0;
-    }
-  }
-  return s;
-}
-
-// s - sum A(j) * B(j), j ascending (s -= a*b per element)
-template <int kU, class FA, class FB>
-__device__ __forceinline__ double seq_fms_up(double s, int j0, int j1, FA A, FB B) {
-  if constexpr (kU == 1) {
-    for (int j = j0; j < j1; j++) s -= A(j) * B(j);
-    return s;
-  }
-  int jb = j0;
-  for (; jb + kU <= j1; jb += kU) {
-    double va[kU], vb[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      va[u] = A(jb + u);
-      vb[u] = B(jb + u);
-    }
-#pragma unroll
-    for (int u = 0; u < kU; u++) s -= va[u] * vb[u];
-  }
-  if (jb < j1) {
-    double va[kU], vb[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      va[u] = jb + u < j1 ? A(jb + u) : 0.0;
-      vb[u] = jb + u < j1 ? B(jb + u) : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; u++)
-      if (jb + u < j1) s -= va[u] * vb[u];
-  }
-  return s;
-}
-
-// s - sum A(k) * B(k), k DEscending from k1-1 down to k0 (s -= a*b per element)
-template <int kU, class FA, class FB>
-__device__ __forceinline__ double seq_fms_down(double s, int k0, int k1, FA A, FB B) {
-  if constexpr (kU == 1) {
-    for (int k = k1 - 1; k >= k0; k--) s -= A(k) * B(k);
-    return s;
-  }
-  int kb = k1 - 1;
-  for (; kb - kU + 1 >= k0; kb -= kU) {
-    double va[kU], vb[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      va[u] = A(kb - u);
-      vb[u] = B(kb - u);
-    }
-#pragma unroll
-    for (int u = 0; u < kU; u++) s -= va[u] * vb[u];
-  }
-  if (kb >= k0) {
-    double va[kU], vb[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      va[u] = kb - u >= k0 ? A(kb - u) : 0.0;
-      vb[u] = kb - u >= k0 ? B(kb - u) : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; u++)
-      if (kb - u >= k0) s -= va[u] * vb[u];
-  }
-  return s;
-}
 
 // Value of v held by lane i of this thread's subgroup (S = 16 / 32: lane i of each 16- / 32-lane group of the wave
 // serve the two QPs; S = 64: lane i).  i must be wave-uniform (a compile-time step index): two
@@ -421,10 +363,25 @@ __device__ __forceinline__ int rpk(int i, int j, int n) {
 // The workspace variant (GJR, 256-thread one-QP workgroups) is held to 128 VGPRs (four waves
 // per SIMD = four resident QPs per CU): its loop is bound by HBM traffic, which it overlaps only
 // across resident QPs (measured: two per CU 399 ms, four 323 ms for C5, profiles/r02_f).
-template <int S, int NMAX, int MMAX, bool GJR, int OCC = 1>
-__global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
-    qp_wave_kernel(const QpArgs a, double* __restrict__ ws) {
+// The solve of one block's QPs.  F: the fast build's arithmetic (wdiv / wdist / wrcp above); the
+// IEEE forms otherwise (the exact build always; the fast build's fallback).  Returns false as
+// soon as a fast form was not valid on some lane of the wave (checked after the equality phase,
+// at every pass of the loop and before the outputs): x, f, status and iters are then not
+// written, and the kernel re-solves the block with the IEEE forms — which also rewrites the
+// m = 0 snapshot (x_eq / f_eq / st_eq) this attempt may have written.  (With -ffp-contract=fast
+// the fallback's multiply-adds are fused too: within 1e-10, not bitwise.)
+template <int S, int NMAX, int MMAX, bool GJR, int OCC, bool F>
+__device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ ws) {
+  static_assert(!F || (!GJR && S <= 64), "the fast build covers the one-wave LDS variants");
   using C = WaveCfg<S, NMAX, MMAX, GJR>;
+  bool fok = true;  // F: every fast form this lane evaluated so far was in range
+  // (one-wave blocks: a ballot is the block-wide OR)
+  auto any_bad = [&]() -> bool {
+    if constexpr (F)
+      return __builtin_amdgcn_ballot_w64(!fok) != 0;
+    else
+      return false;
+  };
   constexpr bool kRegSetup = QPGPU_WAVE_REGSETUP && !GJR && NMAX <= S &&
                              ((S == 32 && OCC == 1) || (S == 16 && OCC <= 2));
   // R packed (upper triangle + subdiagonal) with J still in LDS: less LDS per QP, more resident
@@ -579,7 +536,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
             bad = sd;
           } else {
             const double dg = sqrt(sd);
-            const double v = (j == i) ? dg : sum / dg;
+            const double v = (j == i) ? dg : wdiv<F>(sum, dg, fok);
             if (mine && j >= i) {
               A[i] = v;
               L_(j, i) = v;
@@ -620,7 +577,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         for (int j = i + 1 + ls; j < n; j += S) {
           const double s2 = seq_fms_down<GJR ? kUG : kUL>(L_(i, j), 0, i, [&](int k) { return L_(i, k); },
                                          [&](int k) { return L_(j, k); });
-          L_(j, i) = s2 / dg;
+          L_(j, i) = wdiv<F>(s2, dg, fok);
         }
         if (lead) L_(i, i) = dg;
         grp_sync<S>();
@@ -658,7 +615,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           double lc[NMAX];
 #pragma unroll
           for (int k = 0; k < NMAX; k++) lc[k] = Lq[k];
-          const double y = w[0] / lc[0];
+          const double y = wdiv<F>(w[0], lc[0], fok);
           if (mine) J_(j, q) = y;
 #pragma unroll
           for (int k = 0; k + 1 < NMAX; k++) w[k] = w[k + 1] - lc[k + 1] * y;
@@ -672,10 +629,11 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       // factor array holds both L[j][q] (q < j) and U[j][i] (i > j).  Divisors broadcast with
       // v_readlane.
       const double diag = L_(jc, jc);
+      const double rdiag = F ? wrcp(diag) : 0.0;
       double yv = zv[jc];
       for (int q = 0; q < n; q++) {
         const double lq = L_(jc, q);
-        const double yq = sg_bcast<S>(yv / diag, q);
+        const double yq = sg_bcast<S>(wdiv_r<F>(yv, diag, rdiag, fok), q);
         const double upd = yv - lq * yq;
         yv = (j == q) ? yq : ((j > q) ? upd : yv);
       }
@@ -691,7 +649,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         double v = yv;
 #pragma unroll
         for (int k = i + 1; k < NMAX; k++) v -= P[k];
-        const double xi = sg_bcast<S>(v / diag, i);
+        const double xi = sg_bcast<S>(wdiv_r<F>(v, diag, rdiag, fok), i);
         xm = (j == i) ? xi : xm;
         P[i] = (j < i && i < n) ? Lr[i] * xi : 0.0;
       }
@@ -732,7 +690,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         for (int i = i0; i < n; i++) {
           const double v = seq_fms_up<GJR ? kUG : kUL>((i == r) ? 1.0 : 0.0, i0, i, [&](int j) { return L_(i, j); },
                                       [&](int j) { return J_(r, j); });
-          J_(r, i) = v / L_(i, i);
+          J_(r, i) = wdiv<F>(v, L_(i, i), fok);
         }
       }
       grp_sync<S>();
@@ -744,12 +702,12 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         for (int i = 0; i < n; i++) {
           const double v = seq_fms_up<GJR ? kUG : kUL>(zv[i], 0, i, [&](int j) { return L_(i, j); },
                                       [&](int j) { return dv[j]; });
-          dv[i] = v / L_(i, i);
+          dv[i] = wdiv<F>(v, L_(i, i), fok);
         }
         for (int i = n - 1; i >= 0; i--) {
           const double v = seq_fms_up<GJR ? kUG : kUL>(dv[i], i + 1, n, [&](int j) { return L_(i, j); },
                                       [&](int j) { return xv[j]; });
-          xv[i] = v / L_(i, i);
+          xv[i] = wdiv<F>(v, L_(i, i), fok);
         }
         double f = 0.0;
         for (int i = 0; i < n; i++) {
@@ -901,7 +859,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         auto rowp = [&](int i) -> const double* {
           return kPackedR ? Rm + (i * n - (i * (i - 1)) / 2 - i) : Rm + i * JS;
         };
-        double nd, nRii, nR1, nR[U], nr[U];  // the next row's values
+        double nd, nRii, nrRii, nR1, nR[U], nr[U];  // the next row's values (nrRii: F, 1 / R[i][i])
         // row i's base pointer (Ri[j] = R[i][j]), stepped per row: packed, row i-1 starts
         // n - i entries before row i (no multiplications in the loop)
         const double* Rp = rowp(iq - 1);
@@ -909,6 +867,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           const double* Ri = Rp;
           nd = dv[i];
           nRii = Ri[i];
+          nrRii = F ? wrcp(nRii) : 0.0;  // off the chain: R[i][i] is known before r[i+1]
           nR1 = Ri[i + 1];
 #pragma unroll
           for (int u = 0; u < U; u++) {
@@ -920,8 +879,8 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         double rn;  // r[i+1]
         {
           // row iq-1: an empty sum (+0.0)
-          const double di = nd, Rii = nRii;
-          const double r = (di - 0.0) / Rii;
+          const double di = nd, Rii = nRii, rRii = nrRii;
+          const double r = wdiv_r<F>(di - 0.0, Rii, rRii, fok);
           if (iq > 1) Rp -= kPackedR ? n - (iq - 1) : JS;
           prefetch(iq > 1 ? iq - 2 : 0);
           rv[iq - 1] = r;
@@ -930,7 +889,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         // rows in two runs: chunk 0 partly past the row (c = iq-i-2 < U: masked), then whole
         // (c >= U: unmasked, longer rows' further chunks with the last one masked)
         auto row = [&](int i, auto Whole) {
-          const double di = nd, Rii = nRii, R1 = nR1;
+          const double di = nd, Rii = nRii, rRii = nrRii, R1 = nR1;
           double cR[U], cr[U];
 #pragma unroll
           for (int u = 0; u < U; u++) {
@@ -967,7 +926,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
               }
             }
           }
-          const double r = (di - s) / Rii;
+          const double r = wdiv_r<F>(di - s, Rii, rRii, fok);
           if (i > 0) Rp -= kPackedR ? n - i : JS;
           prefetch(i > 0 ? i - 1 : 0);  // r[i+1 ..] are in LDS already; r[i] is carried
           rv[i] = r;
@@ -984,7 +943,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           const double* Ri = kPackedR ? Rm + (i * n - (i * (i - 1)) / 2 - i) : Rm + i * JS;
           const double s = seq_fma_up<kUL>(0.0, i + 1, iq, [&](int j) { return Ri[j]; },
                                       [&](int j) { return rv[j]; });
-          rv[i] = (dv[i] - s) / Ri[i];
+          rv[i] = wdiv<F>(dv[i] - s, Ri[i], fok);
         }
     } else {
       if (ls >= 64) return;  // waves 1.. idle (they wait at the caller's grp_sync)
@@ -1138,7 +1097,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
 #pragma unroll
           for (int u = 0; u < U; u++) {
             const double a0 = ac[u];
-            const double h = qp_distance(a0, carried);
+            const double h = wdist<F>(a0, carried, fok);
             const bool skip = fabs(h) < kEps;
             GF_(ng + u) = skip ? 0.0 : 1.0;
             GX_(ng + u) = h;
@@ -1148,7 +1107,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         }
         for (; jb >= iq + 1; jb--) {
           const double a0 = dv[jb - 1];
-          const double h = qp_distance(a0, carried);
+          const double h = wdist<F>(a0, carried, fok);
           const bool skip = fabs(h) < kEps;
           GF_(ng) = skip ? 0.0 : 1.0;
           GX_(ng) = h;
@@ -1166,7 +1125,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           for (int u = 0; u < U; u++)
             if (jb - u >= iq + 1) {
               const double a0 = ac[u];
-              const double h = qp_distance(a0, carried);
+              const double h = wdist<F>(a0, carried, fok);
               const bool skip = fabs(h) < kEps;
               GF_(ng) = skip ? 0.0 : 1.0;
               GX_(ng) = h;
@@ -1188,12 +1147,18 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       const int j = n - 1 - gm;
       const double h = GX_(gm), cc_raw = dv[j - 1], dj = dv[j], hp = GX_(gp);
       const bool prev = gm > 0 && GF_(gp) != 0.0, app = GF_(gm) != 0.0;
-      const double ss_raw = prev ? ((dj / hp < 0.0) ? -hp : hp) : dj;
-      double ss1 = ss_raw / h, cc1 = cc_raw / h;
+      // (F: hp > 0 for an applied previous step, so dj / hp < 0 is dj < 0; only applied
+      // rotations of this QP count for the range checks)
+      bool rok = true;
+      const bool dneg = F ? (dj < 0.0) : (dj / hp < 0.0);
+      const double ss_raw = prev ? (dneg ? -hp : hp) : dj;
+      const double rh = F ? wrcp(h) : 0.0;
+      double ss1 = wdiv_r<F>(ss_raw, h, rh, rok), cc1 = wdiv_r<F>(cc_raw, h, rh, rok);
       const bool neg = cc1 < 0.0;
       cc1 = neg ? -cc1 : cc1;
       ss1 = neg ? -ss1 : ss1;
-      const double x1 = ss1 / (1.0 + cc1);
+      const double x1 = wdiv<F>(ss1, 1.0 + cc1, rok);
+      if (F && mine && app) fok = fok && rok;
       const double cc = app ? cc1 : 0.0, ss = app ? ss1 : 0.0, xny = app ? x1 : 0.0;
       const double dlast = app ? (neg ? -h : h) : cc_raw;
       grp_sync<S>();
@@ -1372,13 +1337,14 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       if (iq > 0) {
         for (int j = qq; j < iq; j++) {
           double cc = R_(j, j), ss = R_(j + 1, j);
-          const double h = qp_distance(cc, ss);
+          const double h = wdist<F>(cc, ss, fok);
           if (fabs(h) < kEps) {
             GF_(ng++) = 0.0;
             continue;
           }
-          cc = cc / h;
-          ss = ss / h;
+          const double rh = F ? wrcp(h) : 0.0;
+          cc = wdiv_r<F>(cc, h, rh, fok);
+          ss = wdiv_r<F>(ss, h, rh, fok);
           R_(j + 1, j) = 0.0;
           if (cc < 0.0) {
             R_(j, j) = -h;
@@ -1387,7 +1353,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
           } else {
             R_(j, j) = h;
           }
-          const double xny = ss / (1.0 + cc);
+          const double xny = wdiv<F>(ss, 1.0 + cc, fok);
           for (int k = j + 1; k < iq; k++) {
             const double t1 = R_(j, k), t2 = R_(j + 1, k);
             const double r1 = t1 * cc + t2 * ss;
@@ -1475,7 +1441,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
         const int iq = ctl->iq;
         double t2 = 0.0, zz, znp, npx;
         dot2_lead(zz, znp, &npx);  // np.x in the same pass (the reference's np.x, i ascending)
-        if (fabs(zz) > kEps) t2 = (-npx - c0) / znp;
+        if (fabs(zz) > kEps) t2 = wdiv<F>(-npx - c0, znp, fok);
         ctl->t2 = t2;
         uv[iq] = t2;
         ctl->f += 0.5 * (t2 * t2) * znp;
@@ -1517,6 +1483,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   }
 
   qp_stamp(a, 3);
+  if (any_bad()) return false;  // the fast attempt's setup / equality phase went out of range
   // ------------------------------------------------------------------ active-set loop
   // Per-subgroup state machine; a wave loops until all of its QPs are done.
   const int max_steps = a.max_steps;
@@ -1530,6 +1497,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
   // so two QPs of a wave at different phases share the later blocks instead of running them in
   // separate passes.
   while (true) {
+    if (any_bad()) return false;
     int phase = ctl->phase;
     if (S < 64) {
       if (__builtin_amdgcn_ballot_w64(phase != PH_DONE) == 0) break;
@@ -1755,7 +1723,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       const int iq = ctl->iq;
       for (int k = p + ls; k < iq; k += S)
         if (rv[k] > 0.0) {
-          const double q = uv[k] / rv[k];
+          const double q = wdiv<F>(uv[k], rv[k], fok);
           if (q < t1best) {
             t1best = q;
             kbest = k;
@@ -1782,7 +1750,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
       double t2, zz, znp;
       dot2_lead(zz, znp);
       if (fabs(zz) > kEps) {
-        t2 = -sv[ctl->ip] / znp;
+        t2 = wdiv<F>(-sv[ctl->ip], znp, fok);
         if (t2 < 0) t2 = inf;  // Takano Akio patch
       } else {
         t2 = inf;
@@ -1890,6 +1858,7 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
     for (int k = 3; k < 5; k++) a.stamps[(uint64_t)blockIdx.x * kStampSlots + 11 + k] = teq[k];
   }
   // ------------------------------------------------------------------ outputs
+  if (any_bad()) return false;
   if (live) {
     const int st = ctl->status;
     if (st != QPGPU_QP_NOT_POSITIVE_DEFINITE) {
@@ -1903,6 +1872,20 @@ __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
     }
   }
 #undef EL
+  return true;
+}
+
+template <int S, int NMAX, int MMAX, bool GJR, int OCC = 1>
+__global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
+    QP_WAVE_KERNEL(const QpArgs a, double* __restrict__ ws) {
+  if constexpr (kWaveFast && !GJR && S <= 64) {
+    if (!wave_body<S, NMAX, MMAX, GJR, OCC, true>(a, ws)) {
+      __syncthreads();  // the fast attempt's LDS traffic is over
+      wave_body<S, NMAX, MMAX, GJR, OCC, false>(a, ws);
+    }
+  } else {
+    wave_body<S, NMAX, MMAX, GJR, OCC, false>(a, ws);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1919,14 +1902,14 @@ static hipError_t launch_wave(const QpArgs& a, hipStream_t stream, double* ws) {
   // (OCC 2 for S = 16, OCC 1) use the packed-R layout when QPGPU_WAVE_RPACK is on.
   if constexpr (S < 64 && !GJR) {
     if (lds_bytes <= 20480) {
-      hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR, 4>), dim3((unsigned)blocks), dim3(C::BS),
+      hipLaunchKernelGGL((QP_WAVE_KERNEL<S, NMAX, MMAX, GJR, 4>), dim3((unsigned)blocks), dim3(C::BS),
                          lds_bytes, stream, a, ws);
       return hipGetLastError();
     }
     const size_t lds_p = (size_t)C::QPB * wave_lay(a.n, a.m, GJR, QPGPU_WAVE_RPACK != 0).stride * sizeof(double);
     // four-QP waves (S = 16): up to 40 KiB per block still leaves room for two waves per SIMD
     if (S == 16 && lds_bytes <= 40960) {
-      hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR, 2>), dim3((unsigned)blocks), dim3(C::BS),
+      hipLaunchKernelGGL((QP_WAVE_KERNEL<S, NMAX, MMAX, GJR, 2>), dim3((unsigned)blocks), dim3(C::BS),
                          lds_p, stream, a, ws);
       return hipGetLastError();
     }
@@ -1943,12 +1926,12 @@ static hipError_t launch_wave(const QpArgs& a, hipStream_t stream, double* ws) {
   static size_t granted = 0;  // dynamic LDS beyond 64 KiB must be granted per kernel
   if (lds_bytes > 65536 && lds_bytes > granted) {
     const hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&qp_wave_kernel<S, NMAX, MMAX, GJR>),
+        reinterpret_cast<const void*>(&QP_WAVE_KERNEL<S, NMAX, MMAX, GJR>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
     if (e != hipSuccess) return e;
     granted = lds_bytes;
   }
-  hipLaunchKernelGGL((qp_wave_kernel<S, NMAX, MMAX, GJR>), dim3((unsigned)blocks), dim3(C::BS), lds_bytes,
+  hipLaunchKernelGGL((QP_WAVE_KERNEL<S, NMAX, MMAX, GJR>), dim3((unsigned)blocks), dim3(C::BS), lds_bytes,
                      stream, a, ws);
   return hipGetLastError();
 }
@@ -1960,17 +1943,24 @@ struct WaveVariant {
   hipError_t (*launch)(const QpArgs&, hipStream_t, double*);
 };
 
+#if QPGPU_WAVE_FAST
+#define QPK_WAVE_VNAME(s) "qp_wave_fast<" s ">"
+#else
+#define QPK_WAVE_VNAME(s) "qp_wave<" s ">"
+#endif
 static const WaveVariant kWaveVariants[] = {
 #if QPGPU_WAVE_S16
-    {16, 32, 0, "qp_wave<S=16,N=16,M=32>", launch_wave<16, 16, 32, false>},
+    {16, 32, 0, QPK_WAVE_VNAME("S=16,N=16,M=32"), launch_wave<16, 16, 32, false>},
 #endif
-    {32, 64, 0, "qp_wave<S=32,N=32,M=64>", launch_wave<32, 32, 64, false>},
-    {32, 128, 0, "qp_wave<S=32,N=32,M=128>", launch_wave<32, 32, 128, false>},
-    {64, 128, 0, "qp_wave<S=64,N=64,M=128>", launch_wave<64, 64, 128, false>},
-    {64, 256, 0, "qp_wave<S=64,N=64,M=256>", launch_wave<64, 64, 256, false>},
+    {32, 64, 0, QPK_WAVE_VNAME("S=32,N=32,M=64"), launch_wave<32, 32, 64, false>},
+    {32, 128, 0, QPK_WAVE_VNAME("S=32,N=32,M=128"), launch_wave<32, 32, 128, false>},
+    {64, 128, 0, QPK_WAVE_VNAME("S=64,N=64,M=128"), launch_wave<64, 64, 128, false>},
+    {64, 256, 0, QPK_WAVE_VNAME("S=64,N=64,M=256"), launch_wave<64, 64, 256, false>},
+#if !QPGPU_WAVE_FAST
     {256, 1024, WaveCfg<256, 256, 1024, true>::WS_DOUBLES,
      "qp_panel<MFMA f64 16x16x4> + qp_wave<S=256,N=256,M=1024,global J/R>",
      launch_wave<256, 256, 1024, true>},
+#endif
 };
 
 const WaveVariant* pick_wave(int n, int m) {
@@ -1979,8 +1969,27 @@ const WaveVariant* pick_wave(int n, int m) {
   return nullptr;
 }
 
-}  // namespace qpk
+}  // namespace QPK_WAVE_NS
 
+#if QPGPU_WAVE_FAST
+// the fast build covers the LDS variants only (n <= 64, m <= 256); wider shapes keep the
+// default path (its n > 64 form is already the 1e-10 tolerance mode)
+extern "C" const char* qpk_medium_name_fast(int n, int /*p*/, int m) {
+  const qpk_wfast::WaveVariant* v = qpk_wfast::pick_wave(n, m);
+  return v ? v->name : nullptr;
+}
+extern "C" hipError_t qpk_launch_medium_fast(const qpk::QpArgs* a, hipStream_t stream, int* handled,
+                                             const char** name) {
+  const qpk_wfast::WaveVariant* v = qpk_wfast::pick_wave(a->n, a->m);
+  if (!v) {
+    *handled = 0;
+    return hipSuccess;
+  }
+  *handled = 1;
+  if (name) *name = v->name;
+  return v->launch(*a, stream, nullptr);
+}
+#else
 extern "C" const char* qpk_medium_name(int n, int /*p*/, int m) {
   const qpk::WaveVariant* v = qpk::pick_wave(n, m);
   return v ? v->name : nullptr;
@@ -2021,3 +2030,4 @@ extern "C" hipError_t qpk_launch_medium_ws(const qpk::QpArgs* a, hipStream_t str
   }
   return v->launch(*a, stream, ws);
 }
+#endif  // QPGPU_WAVE_FAST

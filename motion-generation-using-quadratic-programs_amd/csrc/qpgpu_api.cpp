@@ -28,6 +28,13 @@ extern "C" hipError_t qpk_launch_medium_ws(const qpk::QpArgs* a, hipStream_t str
                                            const char** name, double* ws);
 extern "C" int64_t qpk_medium_workspace_bytes(int n, int m, int64_t batch);
 extern "C" const char* qpk_medium_name(int n, int p, int m);
+extern "C" const char* qpk_medium_name_fast(int n, int p, int m);
+extern "C" int qpk_generic_covers(int n, int m);
+extern "C" int64_t qpk_generic_workspace_bytes(int n, int m, int64_t batch);
+extern "C" const char* qpk_generic_name(int n, int p, int m);
+extern "C" hipError_t qpk_launch_generic(const qpk::QpArgs* a, hipStream_t stream, double* ws);
+extern "C" hipError_t qpk_launch_medium_fast(const qpk::QpArgs* a, hipStream_t stream, int* handled,
+                                             const char** name);
 extern "C" int qpk_medium_max_n(void);
 extern "C" int qpk_medium_max_m(void);
 extern "C" hipError_t qpk_relayout(int64_t batch, int E, const double* src, double* dst,
@@ -48,18 +55,24 @@ int hip_fail(hipError_t e, const char* what) {
 // input and is far above any count seen on terminating problems.
 int default_max_steps(int n, int p, int m) { return 1000 + 100 * (n + p + m); }
 
+// The flag rules of include/qpgpu.h: known bits only, FAST excludes EXACT and WRITE_FACTOR, at
+// most one forced family.  Shared by validate() and qpgpu_kernel_name_flags().
+bool flags_valid(uint32_t flags) {
+  const uint32_t fam = QPGPU_FLAG_FORCE_LANE | QPGPU_FLAG_FORCE_SUBGROUP | QPGPU_FLAG_FORCE_WAVE |
+                       QPGPU_FLAG_FORCE_GENERIC;
+  const uint32_t known = QPGPU_FLAG_WRITE_FACTOR | QPGPU_FLAG_EXACT | QPGPU_FLAG_FAST | fam;
+  if (flags & ~known) return false;
+  if ((flags & QPGPU_FLAG_FAST) && (flags & (QPGPU_FLAG_EXACT | QPGPU_FLAG_WRITE_FACTOR))) return false;
+  const uint32_t f = flags & fam;
+  return (f & (f - 1)) == 0;
+}
+
 int validate(const qpgpu_problem_desc* d) {
   if (!d) return QPGPU_ERR_INVALID_ARGUMENT;
   if (d->n <= 0 || d->p < 0 || d->m < 0 || d->batch < 0) return QPGPU_ERR_INVALID_ARGUMENT;
   if (d->layout != QPGPU_LAYOUT_QP_MAJOR && d->layout != QPGPU_LAYOUT_TILED64)
     return QPGPU_ERR_INVALID_ARGUMENT;
-  const uint32_t fam = QPGPU_FLAG_FORCE_LANE | QPGPU_FLAG_FORCE_SUBGROUP | QPGPU_FLAG_FORCE_WAVE;
-  const uint32_t known = QPGPU_FLAG_WRITE_FACTOR | QPGPU_FLAG_EXACT | QPGPU_FLAG_FAST | fam;
-  if (d->flags & ~known) return QPGPU_ERR_INVALID_ARGUMENT;
-  if ((d->flags & QPGPU_FLAG_FAST) && (d->flags & (QPGPU_FLAG_EXACT | QPGPU_FLAG_WRITE_FACTOR)))
-    return QPGPU_ERR_INVALID_ARGUMENT;
-  const uint32_t f = d->flags & fam;
-  if (f & (f - 1)) return QPGPU_ERR_INVALID_ARGUMENT;  // at most one family
+  if (!flags_valid(d->flags)) return QPGPU_ERR_INVALID_ARGUMENT;
   return QPGPU_SUCCESS;
 }
 
@@ -139,10 +152,23 @@ int qpgpu_max_m(void) {
 static bool default_small(int n, int m) { return n <= 8 && m <= 32; }
 
 const char* qpgpu_kernel_name_flags(int32_t n, int32_t p, int32_t m, uint32_t flags) {
-  if ((flags & QPGPU_FLAG_FAST) && !(flags & (QPGPU_FLAG_FORCE_SUBGROUP | QPGPU_FLAG_FORCE_WAVE)) && n > 0 && p >= 0 && m >= 0) {
-    const char* s = qpk_lane_name_fast(n, p, m);
+  if (!flags_valid(flags)) return "";  // the launch would be rejected (QPGPU_ERR_INVALID_ARGUMENT)
+  if ((flags & QPGPU_FLAG_FAST) && n > 0 && p >= 0 && m >= 0) {
+    // the fast builds: the lane kernel's where it covers the shape, else the wave kernel's LDS
+    // variants (n <= 64, m <= 256); a forced family keeps to that family
+    const bool lane_ok = !(flags & (QPGPU_FLAG_FORCE_SUBGROUP | QPGPU_FLAG_FORCE_WAVE));
+    const char* s = lane_ok ? qpk_lane_name_fast(n, p, m) : nullptr;
+    if (s) return s;
+    const bool wave_ok = (flags & QPGPU_FLAG_FORCE_WAVE) ||
+                         (!(flags & (QPGPU_FLAG_FORCE_LANE | QPGPU_FLAG_FORCE_SUBGROUP)) &&
+                          !qpk_lane_name(n, p, m) && !(default_small(n, m) && qpk_small_name(n, p, m)));
+    s = wave_ok ? qpk_medium_name_fast(n, p, m) : nullptr;
     if (s) return s;
   }
+  if (flags & QPGPU_FLAG_FORCE_LANE) return qpk_lane_name(n, p, m) ? qpk_lane_name(n, p, m) : "";
+  if (flags & QPGPU_FLAG_FORCE_SUBGROUP) return qpk_small_name(n, p, m) ? qpk_small_name(n, p, m) : "";
+  if (flags & QPGPU_FLAG_FORCE_WAVE) return qpk_medium_name(n, p, m) ? qpk_medium_name(n, p, m) : "";
+  if (flags & QPGPU_FLAG_FORCE_GENERIC) return qpk_generic_name(n, p, m) ? qpk_generic_name(n, p, m) : "";
   return qpgpu_kernel_name(n, p, m);
 }
 
@@ -153,6 +179,8 @@ const char* qpgpu_kernel_name(int32_t n, int32_t p, int32_t m) {
   s = default_small(n, m) ? qpk_small_name(n, p, m) : nullptr;
   if (s) return s;
   s = qpk_medium_name(n, p, m);
+  if (s) return s;
+  s = qpk_generic_name(n, p, m);  // any other shape (n > 256 or m > 1024)
   return s ? s : "";
 }
 
@@ -224,14 +252,29 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
   if (((reinterpret_cast<uintptr_t>(CI) | reinterpret_cast<uintptr_t>(ci0)) & 15u) == 0)
     a.flags |= qpk::kArgAligned16;
   auto launch_wave = [&]() -> int {
+    if (fast) {
+      e = qpk_launch_medium_fast(&a, s, &handled, nullptr);  // LDS variants (n <= 64, m <= 256)
+      if (handled) return QPGPU_SUCCESS;
+    }
     double* ws = nullptr;
     const int wrc = device_workspace(qpk_medium_workspace_bytes(a.n, a.m, a.batch), s, &ws);
     if (wrc) return wrc;
     e = qpk_launch_medium_ws(&a, s, &handled, nullptr, ws);
     return QPGPU_SUCCESS;
   };
+  auto launch_generic = [&]() -> int {
+    if (!qpk_generic_covers(a.n, a.m)) return QPGPU_SUCCESS;  // handled stays 0
+    double* ws = nullptr;
+    const int wrc = device_workspace(qpk_generic_workspace_bytes(a.n, a.m, a.batch), s, &ws);
+    if (wrc) return wrc;
+    handled = 1;
+    e = qpk_launch_generic(&a, s, ws);
+    return QPGPU_SUCCESS;
+  };
   int wrc = QPGPU_SUCCESS;
-  if (d->flags & QPGPU_FLAG_FORCE_LANE) {
+  if (d->flags & QPGPU_FLAG_FORCE_GENERIC) {
+    wrc = launch_generic();
+  } else if (d->flags & QPGPU_FLAG_FORCE_LANE) {
     e = launch_lane();
   } else if (d->flags & QPGPU_FLAG_FORCE_SUBGROUP) {
     e = qpk_launch_small(&a, s, &handled, nullptr);
@@ -241,6 +284,7 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
     e = launch_lane();
     if (!handled && default_small(a.n, a.m)) e = qpk_launch_small(&a, s, &handled, nullptr);
     if (!handled) wrc = launch_wave();
+    if (!wrc && !handled) wrc = launch_generic();
   }
   if (wrc) return wrc;
   if (!handled) return QPGPU_ERR_UNSUPPORTED_SHAPE;
@@ -253,6 +297,7 @@ static bool family_covers(uint32_t flags, int n, int p, int m) {
   if (flags & QPGPU_FLAG_FORCE_LANE) return qpk_lane_name(n, p, m) != nullptr;
   if (flags & QPGPU_FLAG_FORCE_SUBGROUP) return qpk_small_name(n, p, m) != nullptr;
   if (flags & QPGPU_FLAG_FORCE_WAVE) return qpk_medium_name(n, p, m) != nullptr;
+  if (flags & QPGPU_FLAG_FORCE_GENERIC) return qpk_generic_covers(n, m) != 0;
   return qpgpu_kernel_name(n, p, m)[0] != 0;
 }
 

@@ -49,8 +49,9 @@ FLAG_FAST = 0x4  # lane-kernel shapes: fused multiply-adds, shared reciprocals (
 FLAG_FORCE_LANE = 0x100
 FLAG_FORCE_SUBGROUP = 0x200
 FLAG_FORCE_WAVE = 0x400
+FLAG_FORCE_GENERIC = 0x800  # any shape: the generic workspace kernel (qp_generic.hip)
 FAMILY_FLAGS = {None: 0, "auto": 0, "lane": FLAG_FORCE_LANE, "subgroup": FLAG_FORCE_SUBGROUP,
-                "wave": FLAG_FORCE_WAVE}
+                "wave": FLAG_FORCE_WAVE, "generic": FLAG_FORCE_GENERIC}
 LAYOUT_QP_MAJOR = 0
 LAYOUT_TILED64 = 1
 LAYOUTS = {None: 0, "qp_major": LAYOUT_QP_MAJOR, "tiled64": LAYOUT_TILED64}
@@ -182,6 +183,28 @@ def from_tiled64(flat: np.ndarray, B: int, shape) -> np.ndarray:
     BB = (B + 63) // 64 * 64
     t = np.asarray(flat).reshape(BB // 64, E, 64).transpose(0, 2, 1).reshape(BB, E)
     return np.ascontiguousarray(t[:B]).reshape((B,) + tuple(shape))
+
+
+def rel_error_per_qp(x, x_ref, f, f_ref, tiny: float = np.finfo(np.float64).tiny):
+    """north_star's parity measure ("primal/objective within 1e-10 relative"), per QP:
+    ex_i = ||x_i - xref_i||_inf / max(||xref_i||_inf, tiny), ef_i = |f_i - fref_i| / max(|fref_i|, tiny).
+    Entries that are equal (inf == inf included) or NaN in both count as 0.  Returns the arrays
+    (ex, ef) so callers can report max, percentiles and the worst QP."""
+    x = np.asarray(x, dtype=np.float64).reshape(len(f), -1)
+    xr = np.asarray(x_ref, dtype=np.float64).reshape(len(f_ref), -1)
+    f = np.asarray(f, dtype=np.float64)
+    fr = np.asarray(f_ref, dtype=np.float64)
+    with np.errstate(invalid="ignore", over="ignore"):
+        dx = np.abs(x - xr)
+        dx[(x == xr) | (np.isnan(x) & np.isnan(xr))] = 0.0
+        nx = np.max(np.abs(np.where(np.isnan(xr), 0.0, xr)), axis=1) if xr.shape[1] else np.zeros(len(xr))
+        ex = (np.max(dx, axis=1) if xr.shape[1] else np.zeros(len(xr))) / np.maximum(nx, tiny)
+        df = np.abs(f - fr)
+        df[(f == fr) | (np.isnan(f) & np.isnan(fr))] = 0.0
+        ef = df / np.maximum(np.abs(np.where(np.isnan(fr), 0.0, fr)), tiny)
+    ex[np.isnan(ex)] = np.inf  # one side NaN only
+    ef[np.isnan(ef)] = np.inf
+    return ex, ef
 
 
 def algorithmic_bytes_per_qp(n: int, p: int, m: int) -> int:

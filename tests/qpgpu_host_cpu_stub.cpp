@@ -26,7 +26,9 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const doubl
   if (!d || d->n <= 0 || d->p < 0 || d->m < 0 || d->batch < 0) return QPGPU_ERR_INVALID_ARGUMENT;
   if (d->layout != QPGPU_LAYOUT_QP_MAJOR) return QPGPU_ERR_INVALID_ARGUMENT;
   const int n = d->n, p = d->p, m = d->m;
-  if (n > 256 || m > 1024) return QPGPU_ERR_UNSUPPORTED_SHAPE;  // the kernels' coverage
+  // the kernels' coverage: any shape up to the generic kernel's indexing limits
+  if ((int64_t)n * n >= ((int64_t)1 << 31) || (int64_t)n * m >= ((int64_t)1 << 31))
+    return QPGPU_ERR_UNSUPPORTED_SHAPE;
   const bool wf = (d->flags & QPGPU_FLAG_WRITE_FACTOR) != 0;
   std::vector<double> g((std::size_t)n * n), xb((std::size_t)n);
   for (int64_t b = 0; b < d->batch; ++b) {

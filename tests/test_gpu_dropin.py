@@ -54,17 +54,19 @@ def _parse(out):
 
 
 @pytest.mark.parametrize("kind,n,p,m", [("general", 7, 6, 14), ("box", 7, 0, 14),
-                                        ("general", 14, 10, 28), ("general", 30, 6, 60)])
+                                        ("general", 14, 10, 28), ("general", 30, 6, 60),
+                                        ("general", 300, 10, 1100), ("general", 512, 0, 64)])
 def test_single_qp_through_cpp_symbol_matches_oracle(gpu, tmp_path, kind, n, p, m):
     """BASELINE config 1: single QPs through the mangled solve_quadprog symbol (ArrayHH
     containers, t() temporaries as src/mgqp.cpp:708 passes them), one call each, bit for bit
-    against the oracle: f, x and the Cholesky factor left in G."""
+    against the oracle: f, x and the Cholesky factor left in G.  The reference takes any size
+    (QuadProg++.hh:69-72): (300, 10, 1100) and (512, 0, 64) go through the generic kernel."""
     import numpy as np
 
     import oracle
     import qpgpu
 
-    pr = qpgpu.make_problems(kind, n, p, m, 0, 48, seed=31)
+    pr = qpgpu.make_problems(kind, n, p, m, 0, 48 if n <= 64 else 2, seed=31)
     path = str(tmp_path / "qps.bin")
     _write_batch(path, pr)
     r = subprocess.run([BIN, "--qp", path], capture_output=True, text=True, timeout=300)

@@ -54,6 +54,25 @@ def test_kernel_coverage_table():
     assert qpgpu.kernel_name(14, 10, 28) != ""
     assert qpgpu.kernel_name(0, 0, 0) == ""
     assert qpgpu.LIB.qpgpu_abi_version() == 1
+    # any size, as the reference (QuadProg++.hh:69-72): beyond the specialised kernels the
+    # generic workspace kernel
+    for shape in ((300, 10, 1100), (512, 0, 64), (100, 20, 1500), (4000, 0, 8)):
+        assert qpgpu.kernel_name(*shape).startswith("qp_generic"), shape
+    assert qpgpu.kernel_name(50000, 0, 1) == ""  # n*n >= 2^31: outside even the generic kernel
+    g = qpgpu.LIB.qpgpu_kernel_name_flags(7, 6, 14, qpgpu.FLAG_FORCE_GENERIC).decode()
+    assert g.startswith("qp_generic")
+
+
+def test_kernel_name_flags_follow_the_flag_rules():
+    """qpgpu_kernel_name_flags names what a launch with those flags runs, and nothing for flag
+    combinations the solve entry points reject."""
+    nm = lambda f: qpgpu.LIB.qpgpu_kernel_name_flags(7, 6, 14, f).decode()
+    assert nm(qpgpu.FLAG_FAST).startswith("qp_lane_fast")
+    assert nm(0) == qpgpu.kernel_name(7, 6, 14)
+    assert nm(qpgpu.FLAG_FAST | qpgpu.FLAG_EXACT) == ""
+    assert nm(qpgpu.FLAG_FAST | qpgpu.FLAG_WRITE_FACTOR) == ""
+    assert nm(qpgpu.FLAG_FORCE_LANE | qpgpu.FLAG_FORCE_WAVE) == ""
+    assert nm(0x8) == ""
 
 
 def test_no_device_fails_loudly():

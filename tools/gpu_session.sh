@@ -25,7 +25,7 @@ run() {
 }
 for s in $STEPS; do
   case $s in
-    pytest) run pytest 900 python -m pytest tests -m gpu -q -rf ;;
+    pytest) run pytest 1200 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     benchfull)
