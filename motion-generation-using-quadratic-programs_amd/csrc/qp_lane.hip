@@ -52,6 +52,7 @@
 #define QPGPU_LANE_STAMPS 1
 #endif
 
+
 namespace QPK_LANE_NS {
 using namespace qpk;
 constexpr bool kFast = QPGPU_LANE_FAST != 0;
@@ -194,7 +195,7 @@ __device__ __forceinline__ double ldistance(double a, double b, bool& ok) {
 // [p, iq) loop of the active-set phase (for n = 7, p = 6 that range holds at most one entry).
 // The solve of one wave's 64 QPs.  SAFE: the IEEE forms of division and distance (the exact
 // build always; the fast build's fallback).  Returns false as soon as a fast form was not
-// valid for some lane (checked after the equality phase and at every loop pass): x, f, status
+// valid for some lane (checked after the equality phase and after the loop): x, f, status
 // and iters are not written then, and the caller re-solves the wave with SAFE, which rewrites
 // everything — including the m = 0 snapshot (x_eq, f_eq, st_eq) the fast attempt may already
 // have written.  In the fast build (-ffp-contract=fast) the SAFE body's multiply-adds are
@@ -889,7 +890,11 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
   // Fast build: a fast form that went out of range in the setup or the equality phase (or
   // non-finite data) sends the wave to the IEEE re-solve now, instead of after a loop that
   // would run on garbage up to the step cap.  (The CE / CI copies into LDS have landed: the
-  // re-solve may restage.)
+  // re-solve may restage.)  The same check at the top of every loop pass was measured to change
+  // results: with it, qp_lane_fast<N=8,M=16> returned x off by up to 4e-2 relative on 4 of 1 001
+  // QPs with the same status and pass counts and no fallback taken (profiles/r04_s2), a
+  // code-generation effect we did not localise — so the loop keeps its single check after the
+  // last pass.
   if constexpr (F) {
     if (wave_any(!fok)) return false;
   }
@@ -1096,9 +1101,6 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
     };
     uint64_t tscan = 0, tsel = 0, nloop = 0, tfirst = 0;  // diagnostic stamps only
     while (wave_any(active)) {
-      if constexpr (F) {
-        if (wave_any(!fok)) return false;  // (as above; the loop issues no LDS-DMA)
-      }
       const uint64_t tl0 = (kStamps && a.stamps) ? __builtin_amdgcn_s_memtime() : 0;
       scan_pass();
       const uint64_t tl1 = (kStamps && a.stamps) ? __builtin_amdgcn_s_memtime() : 0;

@@ -185,11 +185,15 @@ def from_tiled64(flat: np.ndarray, B: int, shape) -> np.ndarray:
     return np.ascontiguousarray(t[:B]).reshape((B,) + tuple(shape))
 
 
-def rel_error_per_qp(x, x_ref, f, f_ref, tiny: float = np.finfo(np.float64).tiny):
+def rel_error_per_qp(x, x_ref, f, f_ref, tiny: float = np.finfo(np.float64).tiny, f_scale=None):
     """north_star's parity measure ("primal/objective within 1e-10 relative"), per QP:
     ex_i = ||x_i - xref_i||_inf / max(||xref_i||_inf, tiny), ef_i = |f_i - fref_i| / max(|fref_i|, tiny).
-    Entries that are equal (inf == inf included) or NaN in both count as 0.  Returns the arrays
-    (ex, ef) so callers can report max, percentiles and the worst QP."""
+    With f_scale (per QP, objective_term_scale()), ef_i is relative to max(|fref_i|, f_scale_i): the
+    magnitude of the objective's terms, which is the scale f is determined to when its two terms
+    cancel.  Entries that are equal (inf == inf included) or NaN in both count as 0.  Returns the
+    arrays (ex, ef) so callers can report max, percentiles and the worst QP."""
+    if len(f) == 0:
+        return np.zeros(0), np.zeros(0)
     x = np.asarray(x, dtype=np.float64).reshape(len(f), -1)
     xr = np.asarray(x_ref, dtype=np.float64).reshape(len(f_ref), -1)
     f = np.asarray(f, dtype=np.float64)
@@ -201,10 +205,27 @@ def rel_error_per_qp(x, x_ref, f, f_ref, tiny: float = np.finfo(np.float64).tiny
         ex = (np.max(dx, axis=1) if xr.shape[1] else np.zeros(len(xr))) / np.maximum(nx, tiny)
         df = np.abs(f - fr)
         df[(f == fr) | (np.isnan(f) & np.isnan(fr))] = 0.0
-        ef = df / np.maximum(np.abs(np.where(np.isnan(fr), 0.0, fr)), tiny)
+        den = np.maximum(np.abs(np.where(np.isnan(fr), 0.0, fr)), tiny)
+        if f_scale is not None:
+            den = np.maximum(den, np.where(np.isfinite(f_scale), f_scale, 0.0))
+        ef = df / den
     ex[np.isnan(ex)] = np.inf  # one side NaN only
     ef[np.isnan(ef)] = np.inf
     return ex, ef
+
+
+def objective_term_scale(G, g0, x):
+    """Per QP, 0.5 |x^T G x| + |g0^T x|: the magnitudes of the two terms whose sum is the objective
+    f = 0.5 x^T G x + g0^T x (G the original matrix, x the reference solution).  When they cancel,
+    f itself is only determined to ~eps times this scale (the reference's own rounding), so the
+    objective's relative error is measured against max(|f|, this)."""
+    G = np.asarray(G, dtype=np.float64)
+    if G.shape[0] == 0:
+        return np.zeros(0)
+    x = np.asarray(x, dtype=np.float64).reshape(G.shape[0], -1)
+    g0 = np.asarray(g0, dtype=np.float64).reshape(G.shape[0], -1)
+    with np.errstate(invalid="ignore", over="ignore"):
+        return 0.5 * np.abs(np.einsum("bi,bij,bj->b", x, G, x)) + np.abs(np.einsum("bi,bi->b", g0, x))
 
 
 def algorithmic_bytes_per_qp(n: int, p: int, m: int) -> int:

@@ -61,6 +61,10 @@ void qpo_op_counts(uint64_t out[4]) {
 #define CNT(mul, add, div, sq) ((void)0)
 #endif
 
+#ifdef QPO_TRACE
+void (*qpo_trace_cb)(int n, const double *x) = 0;
+#endif
+
 /* distance(a, b): overflow-safe hypot, three branches (weak symbol `distance`). */
 static double qpo_distance(double a, double b) {
   double a1 = fabs(a), b1 = fabs(b), t;
@@ -335,6 +339,10 @@ int qpo_solve(int n, int p, int m, double *G, const double *g0, const double *CE
 
 l1:
   iter++;
+#ifdef QPO_TRACE
+  /* tools/lazy_scan_sim.py: x at every l1 pass (a separate build; the oracle has no hook) */
+  if (qpo_trace_cb) qpo_trace_cb(n, x);
+#endif
   for (int i = p; i < iq; i++) {
     ip = A[i];
     iai[ip] = -1;
