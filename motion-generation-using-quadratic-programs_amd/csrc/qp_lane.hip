@@ -58,7 +58,7 @@ using namespace qpk;
 constexpr bool kFast = QPGPU_LANE_FAST != 0;
 constexpr bool kStamps = QPGPU_LANE_STAMPS != 0;
 __device__ __forceinline__ void lstamp(const QpArgs& a, int slot) {
-  if constexpr (kStamps) lstamp(a, slot);
+  if constexpr (kStamps) qp_stamp(a, slot);
 }
 
 template <typename T>
@@ -1100,6 +1100,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
         }
     };
     uint64_t tscan = 0, tsel = 0, nloop = 0, tfirst = 0;  // diagnostic stamps only
+    [[maybe_unused]] uint64_t tdzr = 0, tstep = 0;        // (QPGPU_LANE_STAMPS == 2: l2a split)
     while (wave_any(active)) {
       const uint64_t tl0 = (kStamps && a.stamps) ? __builtin_amdgcn_s_memtime() : 0;
       scan_pass();
@@ -1143,9 +1144,18 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
           status = QPGPU_QP_MAX_ITER;
           active = false;
         } else {
+          [[maybe_unused]] uint64_t ts0 = 0;
+          if constexpr (QPGPU_LANE_STAMPS == 2) ts0 = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
           compute_d();
           update_z(kLo);
           update_r(kLo);
+          if constexpr (QPGPU_LANE_STAMPS == 2) {
+            if (a.stamps) {
+              const double sink = rv[0] + zv[0] + dv[NM - 1];
+              asm volatile("" ::"v"(sink));
+              tdzr += __builtin_amdgcn_s_memtime() - ts0;
+            }
+          }
           int l = 0;
           double t1 = inf;
 #pragma unroll
@@ -1166,57 +1176,68 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
             t2 = inf;
           }
           const double t = (t2 < t1) ? t2 : t1;
-          if (t >= inf) {
+          // The step's four outcomes (infeasible, dual step, full step, partial step) as per-lane
+          // predicates over ONE copy of each piece: a wave whose lanes take different outcomes
+          // executes the union of the pieces, and delete_constraint — which the dual step
+          // (drops l), the degenerate full step (drops ip) and the partial step (drops l) all
+          // need — is the largest of them.  Each lane runs exactly its outcome's operations in
+          // the reference's order (x, f, then u; add_constraint; then the delete; then the
+          // rollback or the s[ip] refresh).
+          const bool infs = t >= inf;
+          const bool dual = !infs && t2 >= inf;
+          const bool prim = !infs && !dual;
+          const bool full = prim && fabs(t - t2) < kEps;
+          const bool part = prim && !full;
+          if (infs) {
             status = QPGPU_QP_INFEASIBLE;
             fval = inf;
             active = false;
-          } else if (t2 >= inf) {  // dual step only
-#pragma unroll
-            for (int k = 0; k < NM; k++)
-              if (k < IQLO || k < iq) uv[k] -= t * rv[k];
-            lput_lo<IQLO>(uv, iq, lsel_lo<IQLO>(uv, iq) + t);
-            act &= ~(1ull << l);
-            delete_constraint(l, kLo);
-            need_scan = need_select = false;
-          } else {
+          }
+          if (prim) {
 #pragma unroll
             for (int k = 0; k < NM; k++) xv[k] += t * zv[k];
             fval += t * znp * (0.5 * t + lsel_lo<IQLO>(uv, iq));
+          }
+          if (dual || prim) {
 #pragma unroll
             for (int k = 0; k < NM; k++)
               if (k < IQLO || k < iq) uv[k] -= t * rv[k];
             lput_lo<IQLO>(uv, iq, lsel_lo<IQLO>(uv, iq) + t);
-            if (fabs(t - t2) < kEps) {  // full step
-              if (!add_constraint(kLo)) {
-                excl |= 1ull << ip;
-                delete_constraint(ip, kLo);
-                act = 0;
-#pragma unroll
-                for (int i = 0; i < NM; i++)
-                  if (i >= p && i < iq) {
-                    Av[i] = aold[i];
-                    uv[i] = uold[i];
-                    act |= 1ull << Av[i];
-                  }
-#pragma unroll
-                for (int i = 0; i < NM; i++) xv[i] = xold[i];
-                need_scan = false;
-                need_select = true;
-              } else {
-                act |= 1ull << ip;
-                need_scan = need_select = true;
-              }
-            } else {  // partial step: drop l, refresh s[ip] = CI[:,ip]^T x + ci0[ip]
-              act &= ~(1ull << l);
-              delete_constraint(l, kLo);
-              double s = 0.0;
-#pragma unroll
-              for (int j = 0; j < NM; j++)
-                if (j < n) s += npv[j] * xv[j];
-              lput_lo<0>(sv, ip, s + ci0ip);
-              need_scan = need_select = false;
+          }
+          bool add_fail = false;
+          if (full) {
+            if (!add_constraint(kLo)) {
+              add_fail = true;
+              excl |= 1ull << ip;
+            } else {
+              act |= 1ull << ip;
+              need_scan = need_select = true;
             }
           }
+          if (dual || part) act &= ~(1ull << l);
+          if (dual || part || add_fail) delete_constraint((dual || part) ? l : ip, kLo);
+          if (add_fail) {  // degenerate: roll back to the l1 state, select again
+            act = 0;
+#pragma unroll
+            for (int i = 0; i < NM; i++)
+              if (i >= p && i < iq) {
+                Av[i] = aold[i];
+                uv[i] = uold[i];
+                act |= 1ull << Av[i];
+              }
+#pragma unroll
+            for (int i = 0; i < NM; i++) xv[i] = xold[i];
+            need_scan = false;
+            need_select = true;
+          }
+          if (part) {  // refresh s[ip] = CI[:,ip]^T x + ci0[ip]
+            double s = 0.0;
+#pragma unroll
+            for (int j = 0; j < NM; j++)
+              if (j < n) s += npv[j] * xv[j];
+            lput_lo<0>(sv, ip, s + ci0ip);
+          }
+          if (dual || part) need_scan = need_select = false;
         }
       }
     }
@@ -1225,6 +1246,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
       a.stamps[(uint64_t)blockIdx.x * kStampSlots + 6] = tsel;
       a.stamps[(uint64_t)blockIdx.x * kStampSlots + 7] = nloop;
       a.stamps[(uint64_t)blockIdx.x * kStampSlots + 8] = tfirst;
+      if constexpr (QPGPU_LANE_STAMPS == 2) a.stamps[(uint64_t)blockIdx.x * kStampSlots + 12] = tdzr;
     }
   }
   lstamp(a, 3);

@@ -42,6 +42,9 @@ asp = s[:, 3] - s[:, 2]
 print(f"  in loop: iterations/wave mean {s[:, 7].mean():.2f} max {s[:, 7].max()}; scan {s[:, 5].mean():.0f} "
       f"select {s[:, 6].mean():.0f} l2a+rest {(asp - s[:, 5] - s[:, 6]).mean():.0f} cycles/wave; "
       f"first scan {s[:, 8].mean():.0f}")
+if (s[:, 12] > 0).any():  # QPGPU_LANE_STAMPS=2 builds: compute_d + update_z + update_r inside l2a
+    print(f"  l2a detail: compute_d + update_z + update_r {s[:, 12].mean():.0f} cycles/wave "
+          f"({s[:, 12].mean() / max(1.0, s[:, 7].mean()):.0f} per iteration)")
 mx = it.max(axis=1)
 print("  l1 passes: lane mean", it.mean(), "wave-max mean", mx.mean(), "max", mx.max())
 for v in sorted(set(mx.tolist())):
