@@ -100,7 +100,8 @@ typedef struct {
   int32_t jac_rows[MGQP_MAX_DOF];
   int32_t jac_cols[MGQP_MAX_DOF];
   int32_t status_len;
-  int32_t reserved;
+  uint32_t solver_flags; /* QPGPU_FLAG_* for the level solves: 0 (bitwise with the host paths) or
+                            QPGPU_FLAG_FAST (the wave kernel's fast build: within 1e-10) */
 } mgqp_device_batch;
 
 /* One control cycle for `b->count` robots entirely on the GPU: builder, per-level QPs, the

@@ -49,6 +49,7 @@ struct Plan {
   const float* h;        // [count][dof]
   const float* inertia;  // [count][dof][dof]
   int32_t status_len;
+  uint32_t solver_flags;  // QPGPU_FLAG_* of the level solves (host side only)
   // limits configuration (already size-normalised on the host, :1113-1117)
   float accP[kMaxDof], accN[kMaxDof], tP[kMaxDof], tN[kMaxDof], sup[kMaxDof], inf[kMaxDof];
 };

@@ -647,6 +647,7 @@ int run_cycle(const Plan& P, int64_t K, const float* Bcumul_host, float* torques
     d.p = p;
     d.m = m;
     d.batch = K;
+    d.flags = P.solver_flags;
     // one launch gives both the solve with CI and the retry without it (:717-736): the latter
     // is the state after the equality phase (qpgpu_solve_batched_eq)
     const int rc = qpgpu_solve_batched_eq(&d, G, g0, CE, ce0, CI, ci0, x1, f1, s1, nullptr, x2,

@@ -43,6 +43,7 @@ int MotionGenerationQuadraticProgram::update_device(const void* batch, float* to
   P.h = b.h;
   P.inertia = b.inertia;
   P.status_len = b.status_len;
+  P.solver_flags = b.solver_flags;
 
   // generators in the reference's order: joints outer, levels inner, task rows before the
   // joint row; the dynamics rows close level 0 (:1136-1143)

@@ -106,7 +106,7 @@ class DeviceBatchC(ctypes.Structure):
                 ("jacobian", _P * MAX_DOF), ("jacobian_dot", _P * MAX_DOF),
                 ("ts_len", ctypes.c_int32 * MAX_DOF), ("jac_rows", ctypes.c_int32 * MAX_DOF),
                 ("jac_cols", ctypes.c_int32 * MAX_DOF), ("status_len", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("solver_flags", ctypes.c_uint32)]
 
 
 class DeviceScenario:
@@ -270,10 +270,13 @@ class Controller:
         return codes, tq, tr
 
 
-def _update_device(self, dsc: "DeviceScenario", out=None, stream=None):
+def _update_device(self, dsc: "DeviceScenario", out=None, stream=None, fast: bool = False):
     """The device-resident cycle (mgqp_update_device).  Returns (rc, codes, torques, tracking)
-    as torch tensors on the scenario's device (enqueued on `stream`, not synchronised)."""
+    as torch tensors on the scenario's device (enqueued on `stream`, not synchronised).
+    fast=True solves the levels with the wave kernel's QPGPU_FLAG_FAST build (1e-10)."""
     import torch
+
+    dsc.c.solver_flags = 0x4 if fast else 0  # QPGPU_FLAG_FAST
 
     dev = next(iter(dsc.tensors.values())).device
     if out is None:

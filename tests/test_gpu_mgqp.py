@@ -235,3 +235,24 @@ def test_device_cycle_early_exits(gpu):
     del sc.ports[(6, "jacobian")]
     rc, _, _, _ = _ctl().update_device(mgqp.DeviceScenario(sc, "cuda"))
     assert rc == mgqp.CYCLE_NO_JACOBIAN
+
+
+def test_device_cycle_fast_solves(gpu):
+    """The device cycle with its level solves on the wave kernel's QPGPU_FLAG_FAST build (the
+    reference's own n = 14 QPs, within 1e-10 in double): the same exits per robot, torques and
+    tracking within the float tolerance of the bitwise cycle."""
+    import torch
+
+    sc = mgqp.make_scenario(700, seed=41)
+    dsc = mgqp.DeviceScenario(sc, "cuda")
+    c = _ctl()
+    rc, codes, tq, tr = c.update_device(dsc)
+    torch.cuda.synchronize()
+    codes, tq, tr = codes.cpu().numpy(), tq.cpu().numpy(), tr.cpu().numpy()
+    rcf, codesf, tqf, trf = _ctl().update_device(dsc, fast=True)
+    torch.cuda.synchronize()
+    assert rc == rcf == 0
+    np.testing.assert_array_equal(codesf.cpu().numpy(), codes)
+    ok = codes == 0
+    _close(tqf.cpu().numpy()[ok], tq[ok])
+    _close(trf.cpu().numpy()[ok], tr[ok])

@@ -43,6 +43,8 @@ def main():
                     help="angle limits +-20 rad and gains (10, 2), as tests/test_gpu_mgqp.py's wide case: "
                          "level-0 QPs are then feasible for part of the robots, so their solves run the "
                          "active-set loop instead of the retry snapshot")
+    ap.add_argument("--fast", action="store_true",
+                    help="level solves with the wave kernel's QPGPU_FLAG_FAST build (within 1e-10)")
     args = ap.parse_args()
 
     def configure(ctl):
@@ -59,21 +61,21 @@ def main():
     outs = []
     for j in range(S):  # one output set per stream (workspaces are per stream in the library)
         with torch.cuda.stream(streams[j]):
-            rc, codes, tq, tr = c.update_device(dsc, stream=streams[j].cuda_stream)
+            rc, codes, tq, tr = c.update_device(dsc, stream=streams[j].cuda_stream, fast=args.fast)
         outs.append((tq, tr, codes))
     for k in range(args.warmup):
-        c.update_device(dsc, out=outs[k % S], stream=streams[k % S].cuda_stream)
+        c.update_device(dsc, out=outs[k % S], stream=streams[k % S].cuda_stream, fast=args.fast)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        c.update_device(dsc, out=outs[k % S], stream=streams[k % S].cuda_stream)
+        c.update_device(dsc, out=outs[k % S], stream=streams[k % S].cuda_stream, fast=args.fast)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / args.steps
     # serialized cycle time (one stream, HIP events)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(streams[0])
     for _ in range(3):
-        c.update_device(dsc, out=outs[0], stream=streams[0].cuda_stream)
+        c.update_device(dsc, out=outs[0], stream=streams[0].cuda_stream, fast=args.fast)
     e1.record(streams[0])
     torch.cuda.synchronize()
     ms_serial = e0.elapsed_time(e1) / 3
@@ -84,7 +86,8 @@ def main():
            "ms_per_step": ms, "ms_per_cycle_serialized": ms_serial, "streams": S,
            "streams_outputs_identical": bool(same), "steps": args.steps, "warmup": args.warmup,
            "written_frac": ok, "dtype": "f32 glue + f64 QPs", "data": "synthetic",
-           "limits": "wide (+-20 rad, gains 10/2)" if args.wide else "ops/mgqp.ops"}
+           "limits": "wide (+-20 rad, gains 10/2)" if args.wide else "ops/mgqp.ops",
+           "level_solves": "fast (QPGPU_FLAG_FAST, 1e-10)" if args.fast else "exact (bitwise)"}
 
     if not args.no_host:
         hs = mgqp.make_scenario(args.host_robots, seed=2026)

@@ -43,6 +43,9 @@ for q in range(Q):
     lib.qpo_solve(n, p, m, P(G), P(pr.g0[q]), None, None, P(np.ascontiguousarray(pr.CI[q])), P(pr.ci0[q]),
                   P(x), P(f), P(it), 100000)
     CI, ci0 = pr.CI[q], pr.ci0[q]
+    if os.environ.get("LAZY_SORT") == "1":  # constraints stored in the order of their first-scan slack
+        order = np.argsort(-(CI.T @ xs[0] + ci0))
+        CI, ci0 = CI[:, order], ci0[order]
     a2 = np.linalg.norm(CI, axis=0)
     a1 = np.abs(CI).sum(axis=0)
     nb = (m + BLK - 1) // BLK
