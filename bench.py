@@ -91,7 +91,7 @@ def parse(argv=None):
                     help="workload (default: C1 on one GPU, C4 on N > 1)")
     ap.add_argument("--batch", type=int, default=0, help="QPs per GPU (default: the config's)")
     ap.add_argument("--seed", type=int, default=2026)
-    ap.add_argument("--family", default=None, choices=["lane", "subgroup", "wave"],
+    ap.add_argument("--family", default=None, choices=["lane", "subgroup", "wave", "generic", "pair"],
                     help="force a kernel family (default: the dispatcher's choice)")
     ap.add_argument("--layout", default="qp_major", choices=["qp_major", "tiled64"],
                     help="batch layout of the resident inputs (include/qpgpu.h)")
@@ -292,10 +292,8 @@ def main():
         scaling = "weak"
     b0, b1 = qpdist.shard(rank, B)
     pr = qpgpu.make_problems(kind, n, p, m, b0, b1, seed=args.seed)
-    kname = qpgpu.kernel_name(n, p, m, fast=args.fast)
-    if args.family:
-        kname = {"lane": f"qp_lane[n={n},m={m}]", "subgroup": f"qp_small[n={n},m={m}]",
-                 "wave": f"qp_wave[n={n},m={m}]"}[args.family]
+    kname = qpgpu.LIB.qpgpu_kernel_name_flags(
+        n, p, m, (qpgpu.FLAG_FAST if args.fast else 0) | qpgpu.FAMILY_FLAGS[args.family]).decode()
     if not kname:
         sys.exit(f"no gfx950 kernel covers (n, p, m) = {(n, p, m)}")
     base = qpgpu.DeviceBatch(pr, dev, with_iters=False, layout=args.layout)

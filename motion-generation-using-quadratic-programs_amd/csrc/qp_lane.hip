@@ -52,7 +52,6 @@
 #define QPGPU_LANE_STAMPS 1
 #endif
 
-
 namespace QPK_LANE_NS {
 using namespace qpk;
 constexpr bool kFast = QPGPU_LANE_FAST != 0;
@@ -61,30 +60,7 @@ __device__ __forceinline__ void lstamp(const QpArgs& a, int slot) {
   if constexpr (kStamps) qp_stamp(a, slot);
 }
 
-template <typename T>
-__device__ __forceinline__ T opq_l(T v) {
-  asm("" : "+v"(v));
-  return v;
-}
-
-// v[i] / v[i] = x for a run-time i known to be >= LO (entries below LO are never selected)
-template <int LO, int N, typename T>
-__device__ __forceinline__ T lsel_lo(const T (&v)[N], int i) {
-  T r = opq_l(v[LO]);
-#pragma unroll
-  for (int k = LO + 1; k < N; k++) r = (k == i) ? opq_l(v[k]) : r;
-  return r;
-}
-template <int N, typename T>
-__device__ __forceinline__ T lsel(const T (&v)[N], int i) {
-  return lsel_lo<0>(v, i);
-}
-
-template <int LO, int N, typename T>
-__device__ __forceinline__ void lput_lo(T (&v)[N], int i, T x) {
-#pragma unroll
-  for (int k = LO; k < N; k++) v[k] = (k == i) ? x : v[k];
-}
+// opq_l, lsel_lo, lsel, lput_lo, RIdx, wave_any: qp_common.h (shared with qp_pair.hip)
 
 // A double parked in two AGPRs.  VALU cannot operate on AGPRs, but v_accvgpr_read/write move a
 // dword in one issue slot, far cheaper than the L2 / Infinity-Cache round trip the scan would
@@ -109,17 +85,6 @@ __device__ __forceinline__ double from_agpr(const AgprD& a) {
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
-// R storage: packed upper triangle (row-major) followed by the first subdiagonal.
-template <int NM>
-struct RIdx {
-  static constexpr int NUP = NM * (NM + 1) / 2;
-  static constexpr int SIZE = NUP + NM - 1;
-  // compile-time index of R[i][j]; -1 for entries that are always zero
-  static constexpr int at(int i, int j) {
-    return j >= i ? i * NM - i * (i - 1) / 2 + (j - i) : (i == j + 1 ? NUP + j : -1);
-  }
-};
-
 constexpr int kQpw = 64;      // QPs per wave: one per lane
 constexpr int kStage = 5120;  // staging buffer, doubles (40 KiB: 4 waves per CU)
 // The first l1 scan (which fills the on-chip CI copy) is software-pipelined two rows deep: row
@@ -134,62 +99,8 @@ constexpr int kScanDepth = 2;
 #define QPGPU_LANE_DMA_P0 0
 #endif
 
-__device__ __forceinline__ bool wave_any(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
-
-// ---- arithmetic of the fast build.  F (= kFast and not the fallback body) selects the fast
-// forms; otherwise a / b is the IEEE division and distance the reference's scaled form.  The
-// fast forms are valid for operands well inside the exponent range: each one ANDs its own
-// validity into the lane's `ok`, and a wave with any lane not ok re-solves with the IEEE forms
-// (lane_body<..., SAFE = true>), so no branch sits inside the arithmetic.
-// 1 / b: the v_rcp_f64 seed and the two Newton steps of the compiler's own division sequence,
-// without its range scaling and special-case fix-up
-__device__ __forceinline__ double frcp(double b) {
-  double y = __builtin_amdgcn_rcp(b);
-  double e = __builtin_fma(-b, y, 1.0);
-  y = __builtin_fma(y, e, y);
-  e = __builtin_fma(-b, y, 1.0);
-  return __builtin_fma(y, e, y);
-}
-__device__ __forceinline__ bool rcp_ok(double r) {
-  return __builtin_amdgcn_class(r, 0x108);  // +-normal (b zero, denormal, huge, inf or NaN fail)
-}
-// a / b given rb = frcp(b) (F) — a * rb
-template <bool F>
-__device__ __forceinline__ double ldiv_r(double a, double b, double rb, bool& ok) {
-  if constexpr (F) {
-    ok = ok && rcp_ok(rb);
-    return a * rb;
-  } else {
-    return a / b;
-  }
-}
-template <bool F>
-__device__ __forceinline__ double ldiv(double a, double b, bool& ok) {
-  if constexpr (F)
-    return ldiv_r<true>(a, b, frcp(b), ok);
-  else
-    return a / b;
-}
-// distance(a, b) (F): sqrt(a^2 + b^2) with the [1, 2]-free form of sqrt_1to2's refinement,
-// valid for a^2 + b^2 in [2^-600, 2^600] (and exactly 0 when a = b = 0, as the reference's)
-template <bool F>
-__device__ __forceinline__ double ldistance(double a, double b, bool& ok) {
-  if constexpr (F) {
-    const double s = __builtin_fma(a, a, b * b);
-    const double y = __builtin_amdgcn_rsq(s);
-    double g = s * y, h = y * 0.5;
-    const double r = __builtin_fma(-h, g, 0.5);
-    g = __builtin_fma(g, r, g);
-    h = __builtin_fma(h, r, h);
-    const double d = __builtin_fma(-g, g, s);
-    g = __builtin_fma(d, h, g);
-    const bool z = (a == 0.0) && (b == 0.0);
-    ok = ok && (z || (s >= 0x1p-600 && s <= 0x1p600));
-    return z ? 0.0 : g;
-  } else {
-    return qp_distance(a, b);
-  }
-}
+// ---- arithmetic of the fast build (frcp, rcp_ok, ldiv_r, ldiv, ldistance): qp_common.h,
+// shared with the lane-pair kernel (qp_pair.hip).
 
 // PX >= 0: p is the compile-time constant PX as well (C1/C4: 6, C2: 0), which folds every
 // [p, iq) loop of the active-set phase (for n = 7, p = 6 that range holds at most one entry).
@@ -820,13 +731,14 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
             c0_done = true;
           }
         }
-        if (!c0_done)
+        if (!c0_done) {
           if (ce_staged) {
             const double v = rd_all(offc, p, i);
             c0 = live ? v : 0.0;
           } else {
             c0 = live ? view(const_cast<double*>(a.ce0), p)[i * T] : 0.0;
           }
+        }
       } else {  // p > n: the step that reports "dependent" (reference UB, see oracle)
         const double* CEb = view(const_cast<double*>(a.CE), n * p);
 #pragma unroll

@@ -24,6 +24,9 @@ extern "C" const char* qpk_lane_name(int n, int p, int m);
 extern "C" hipError_t qpk_launch_lane_fast(const qpk::QpArgs* a, hipStream_t stream, int* handled,
                                            const char** name);
 extern "C" const char* qpk_lane_name_fast(int n, int p, int m);
+extern "C" hipError_t qpk_launch_pair(const qpk::QpArgs* a, hipStream_t stream, int* handled,
+                                      const char** name);
+extern "C" const char* qpk_pair_name(int n, int p, int m);
 extern "C" hipError_t qpk_launch_medium_ws(const qpk::QpArgs* a, hipStream_t stream, int* handled,
                                            const char** name, double* ws);
 extern "C" int64_t qpk_medium_workspace_bytes(int n, int m, int64_t batch);
@@ -59,10 +62,11 @@ int default_max_steps(int n, int p, int m) { return 1000 + 100 * (n + p + m); }
 // most one forced family.  Shared by validate() and qpgpu_kernel_name_flags().
 bool flags_valid(uint32_t flags) {
   const uint32_t fam = QPGPU_FLAG_FORCE_LANE | QPGPU_FLAG_FORCE_SUBGROUP | QPGPU_FLAG_FORCE_WAVE |
-                       QPGPU_FLAG_FORCE_GENERIC;
+                       QPGPU_FLAG_FORCE_GENERIC | QPGPU_FLAG_FORCE_PAIR;
   const uint32_t known = QPGPU_FLAG_WRITE_FACTOR | QPGPU_FLAG_EXACT | QPGPU_FLAG_FAST | fam;
   if (flags & ~known) return false;
   if ((flags & QPGPU_FLAG_FAST) && (flags & (QPGPU_FLAG_EXACT | QPGPU_FLAG_WRITE_FACTOR))) return false;
+  if ((flags & QPGPU_FLAG_FORCE_PAIR) && !(flags & QPGPU_FLAG_FAST)) return false;  // fast-only family
   const uint32_t f = flags & fam;
   return (f & (f - 1)) == 0;
 }
@@ -153,6 +157,7 @@ static bool default_small(int n, int m) { return n <= 8 && m <= 32; }
 
 const char* qpgpu_kernel_name_flags(int32_t n, int32_t p, int32_t m, uint32_t flags) {
   if (!flags_valid(flags)) return "";  // the launch would be rejected (QPGPU_ERR_INVALID_ARGUMENT)
+  if (flags & QPGPU_FLAG_FORCE_PAIR) return qpk_pair_name(n, p, m) ? qpk_pair_name(n, p, m) : "";
   if ((flags & QPGPU_FLAG_FAST) && n > 0 && p >= 0 && m >= 0) {
     // the fast builds: the lane kernel's where it covers the shape, else the wave kernel's LDS
     // variants (n <= 64, m <= 256); a forced family keeps to that family
@@ -272,7 +277,9 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
     return QPGPU_SUCCESS;
   };
   int wrc = QPGPU_SUCCESS;
-  if (d->flags & QPGPU_FLAG_FORCE_GENERIC) {
+  if (d->flags & QPGPU_FLAG_FORCE_PAIR) {
+    e = qpk_launch_pair(&a, s, &handled, nullptr);
+  } else if (d->flags & QPGPU_FLAG_FORCE_GENERIC) {
     wrc = launch_generic();
   } else if (d->flags & QPGPU_FLAG_FORCE_LANE) {
     e = launch_lane();
@@ -298,6 +305,7 @@ static bool family_covers(uint32_t flags, int n, int p, int m) {
   if (flags & QPGPU_FLAG_FORCE_SUBGROUP) return qpk_small_name(n, p, m) != nullptr;
   if (flags & QPGPU_FLAG_FORCE_WAVE) return qpk_medium_name(n, p, m) != nullptr;
   if (flags & QPGPU_FLAG_FORCE_GENERIC) return qpk_generic_covers(n, m) != 0;
+  if (flags & QPGPU_FLAG_FORCE_PAIR) return qpk_pair_name(n, p, m) != nullptr;
   return qpgpu_kernel_name(n, p, m)[0] != 0;
 }
 

@@ -16,25 +16,27 @@ import qpgpu  # noqa: E402
 kind, n, p, m = (sys.argv[1] if len(sys.argv) > 1 else "general"), 7, 6, 14
 layout = sys.argv[2] if len(sys.argv) > 2 else "qp_major"
 fast = len(sys.argv) > 3 and sys.argv[3] == "fast"
+family = sys.argv[4] if len(sys.argv) > 4 else "lane"  # "pair": 32 QPs per wave (qp_pair.hip)
+QPW = 32 if family == "pair" else 64
 if kind == "box":
     p = 0
 B = 65536
 pr = qpgpu.make_problems(kind, n, p, m, 0, B, seed=2026)
 db = qpgpu.DeviceBatch(pr, "cuda:0", layout=layout)
-waves = (B + 63) // 64
+waves = (B + QPW - 1) // QPW
 st = torch.zeros(waves * 18, dtype=torch.int64, device="cuda:0")
 fn = qpgpu.LIB.qpgpu_debug_set_stamps
 fn.argtypes = [ctypes.c_void_p]
 for rep in range(3):
     fn(ctypes.c_void_p(st.data_ptr()))
-    db.solve(family="lane", fast=fast)
+    db.solve(family=family, fast=fast)
     torch.cuda.synchronize()
 fn(None)
 s = st.cpu().numpy().reshape(waves, 18).astype(np.int64)
-it = db.iters.cpu().numpy()[: waves * 64].reshape(waves, 64)
+it = db.iters.cpu().numpy()[: waves * QPW].reshape(waves, QPW)
 names = ["loads+setup", "equality", "active-set", "stores"]
 tot = s[:, 4] - s[:, 0]
-print(f"{kind} {layout}{' fast' if fast else ''}: total cycles/wave mean {tot.mean():.0f} p50 {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max()}")
+print(f"{kind} {layout}{' fast' if fast else ''} {family}: total cycles/wave mean {tot.mean():.0f} p50 {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max()}")
 for k, nm in enumerate(names):
     d = s[:, k + 1] - s[:, k]
     print(f"  {nm:12s} mean {d.mean():9.0f} p50 {np.median(d):9.0f} p90 {np.percentile(d, 90):9.0f} max {d.max():9d}")
