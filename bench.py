@@ -320,14 +320,15 @@ def main():
 
     launchers = {}
 
-    def launcher(r, j, stream, fast=None):
+    def launcher(r, j, stream, fast=None, family=None):
         fast = args.fast if fast is None else fast
-        key = (r, j, stream.cuda_stream, fast)
+        family = args.family if family is None else family
+        key = (r, j, stream.cuda_stream, fast, family)
         if key not in launchers:
             v = sets[r].__class__.__new__(sets[r].__class__)
             v.__dict__.update(sets[r].__dict__)
             v.x, v.f, v.status = outs[j]
-            launchers[key] = v.launcher(stream, family=args.family, fast=fast)
+            launchers[key] = v.launcher(stream, family=family, fast=fast)
         return launchers[key]
 
     gather = world > 1 and args.gather != "none"
@@ -408,11 +409,11 @@ def main():
     # that stream around each launch, rotating over the cold sets (and once more warm)
     cs = streams[0]
 
-    def kernel_ms(rotate, per_launch=False, fast=None):
+    def kernel_ms(rotate, per_launch=False, fast=None, family=None):
         # one HIP-event pair around kernel_reps back-to-back launches on one stream (average
         # launch-to-launch duration: kernel + the dependent-launch gap), or a pair per launch
         K_ = args.kernel_reps
-        fns = [launcher(q % R if rotate else 0, 0, cs, fast) for q in range(K_)]
+        fns = [launcher(q % R if rotate else 0, 0, cs, fast, family) for q in range(K_)]
         if per_launch:
             st_ = [torch.cuda.Event(enable_timing=True) for _ in range(K_)]
             en_ = [torch.cuda.Event(enable_timing=True) for _ in range(K_)]
@@ -471,6 +472,32 @@ def main():
                  "max_rel_f_vs_terms": (float(efs.max()) if efs is not None and efs.size else None),
                  "rel_err_of": ("the fast build against the exact build, per QP (||dx||_inf/||x||_inf, "
                                 "|df|/|f|, |df|/max(|f|, 0.5|x'Gx|+|g0'x|))")}
+
+    # the lane-pair kernel (qp_pair.hip: one QP per two lanes, two waves per SIMD),
+    # measured beside the line's kernel on the same box: its kernel time and its agreement with
+    # this line's solve of set 0
+    pair_rec = None
+    kname_pair = qpgpu.LIB.qpgpu_kernel_name_flags(n, p, m, qpgpu.FLAG_FAST | qpgpu.FLAG_FORCE_PAIR).decode()
+    if world == 1 and not args.family and args.fast and kname_pair and args.layout == "qp_major":
+        launcher(0, 0, cs, True, "pair")()  # first launch (code-object load)
+        torch.cuda.synchronize(dev)
+        kp = kernel_ms(True, fast=True, family="pair")
+        launcher(0, 0, cs)()
+        torch.cuda.synchronize(dev)
+        mine = [t.clone() for t in outs[0]]
+        launcher(0, 0, cs, True, "pair")()
+        torch.cuda.synchronize(dev)
+        theirs = [t.clone() for t in outs[0]]
+        ok_ = (mine[2] == qpgpu.QP_OK).cpu().numpy()
+        exq, _ = qpgpu.rel_error_per_qp(theirs[0].reshape(B, -1).cpu().numpy()[ok_],
+                                        mine[0].reshape(B, -1).cpu().numpy()[ok_],
+                                        theirs[1].cpu().numpy()[ok_], mine[1].cpu().numpy()[ok_])
+        pair_rec = {"kernel": kname_pair, "kernel_ms": kp, "frac": bpq * B / (kp * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    "status_identical": bool(torch.equal(mine[2], theirs[2])),
+                    "max_rel_x_vs_line": float(exq.max()) if exq.size else 0.0,
+                    "note": "one QP per lane pair, 32 QPs per wave, two waves per SIMD; not the "
+                            "default: its duplicated serial chains cost more than the co-resident "
+                            "wave hides (DESIGN 5.9)"}
 
     gather_ms = gat.time_one() if gat else None  # one step's gather alone, same payload
 
@@ -638,6 +665,8 @@ def main():
     }
     if other:
         out["other_arithmetic"] = other
+    if pair_rec:
+        out["pair_kernel"] = pair_rec
     if gather:
         out["gather_ms"] = gather_ms
         out["gather_bytes_per_rank"] = gat.bytes_per_rank

@@ -30,6 +30,23 @@
 
 #include "qp_common.h"
 
+// A/B knobs (tools/ab_pair.sh): CE loads kCeAhead steps ahead; the CI copy by DMA during the
+// equality phase (1) or by the first scan (0).  Measured on C1 (profiles/r04_s15, r04_s16;
+// kernel us): DMA from step 0 48.7, from step 3 45.6, from step 4 44.5, no DMA 43.8 (the first
+// scan then reads rows 0..4 from memory, +4k cycles per wave, but the equality phase loses the
+// waits on the copy: 16.1k instead of 19.5-31.6k cycles) — so 0.
+#ifndef QPGPU_PAIR_CE_AHEAD
+#define QPGPU_PAIR_CE_AHEAD 2
+#endif
+#ifndef QPGPU_PAIR_DMA
+#define QPGPU_PAIR_DMA 0
+#endif
+// first equality step that issues a part of the CI copy (-1: the step that issues the last CE
+// load, so that no CE load queues behind a copy part)
+#ifndef QPGPU_PAIR_DMA_FROM
+#define QPGPU_PAIR_DMA_FROM -1
+#endif
+
 namespace qpk_pair {
 using namespace qpk;
 
@@ -142,7 +159,7 @@ __device__ __forceinline__ bool pair_body(const QpArgs& a, double* sbuf) {
   };
   // p > 0: the copy by LDS-DMA during the equality phase (16-B pieces: CI 16-B aligned); p = 0:
   // the first scan writes it (qp_lane.hip measured no gain for a DMA without an equality phase)
-  const bool dma = PX > 0 && kCiRows > 0 && (a.flags & kArgAligned16);
+  const bool dma = QPGPU_PAIR_DMA && PX > 0 && kCiRows > 0 && (a.flags & kArgAligned16);
   auto dma_ci_part = [&](int part, int parts) {
     const int per = (kCiInstr + parts - 1) / parts;
     const double* src = a.CI + bs * (int64_t)(NM * MM);
@@ -161,6 +178,7 @@ __device__ __forceinline__ bool pair_body(const QpArgs& a, double* sbuf) {
   [[maybe_unused]] Touch<kCe0B> pf_ce0;
   [[maybe_unused]] Touch<kCiB> pf_ci;
   [[maybe_unused]] Touch<kCi0B> pf_ci0;
+  [[maybe_unused]] Touch<kCiRows * MM * 8> pf_cil;  // without the copy by DMA: the rows it would copy
 
   int status = QPGPU_QP_OK;
   double fval = 0.0;
@@ -170,16 +188,21 @@ __device__ __forceinline__ bool pair_body(const QpArgs& a, double* sbuf) {
   for (int k = 0; k < H; k++) xh[k] = 0.0;
   double c1 = 0.0, c2 = 0.0;
   double Jh[H][NM];  // J, own rows
-  // equality phase operands: np (own rows) and ce0 of the next step, loaded one step ahead
-  [[maybe_unused]] double npn[H], c0n = 0.0;
+  // equality phase operands: np (own rows) and ce0 of step i, loaded kCeAhead steps ahead —
+  // the first kCeAhead right after G has been read, so they arrive during the setup's compute
+  // (one step ahead, every step waited a full memory latency: 39.5k instead of ~20k cycles per
+  // wave, profiles/r04_s13; three or all six ahead spill registers)
+  constexpr int kCeAhead = QPGPU_PAIR_CE_AHEAD;
+  constexpr int PXA = PX > 0 ? PX : 1;
+  [[maybe_unused]] double cea[PXA][H], c0a[PXA];
   const double* CEq = a.CE + bs * (int64_t)(NM * PX) + h * PX;  // row h of this QP's CE
   auto load_ce = [&](int i) {
 #pragma unroll
     for (int k = 0; k < H; k++) {
       const double v = CEq[(has_row(k) ? 2 * k : 0) * PX + i];
-      npn[k] = has_row(k) ? v : 0.0;
+      cea[i][k] = has_row(k) ? v : 0.0;
     }
-    c0n = a.ce0[bs * PX + i];
+    c0a[i] = a.ce0[bs * PX + i];
   };
 
   qp_stamp(a, 0);  // diagnostic phase clocks (tools/stamps.py; a.stamps is NULL in product calls)
@@ -206,11 +229,13 @@ __device__ __forceinline__ bool pair_body(const QpArgs& a, double* sbuf) {
     __syncthreads();  // G read: the LDS is the CI copy's from here
     qp_stamp(a, 9);
     if constexpr (PX > 0) {
-      load_ce(0);
+#pragma unroll
+      for (int i = 0; i < PX && i < kCeAhead; i++) load_ce(i);
       pf_ce.load(a.CE + bs * (int64_t)(NM * PX), h);
       pf_ce0.load(a.ce0 + bs * PX, h);
       pf_ci.load(a.CI + bs * (int64_t)(NM * MM) + kCiRows * MM, h);
       pf_ci0.load(a.ci0 + bs * MM, h);
+      if (!dma) pf_cil.load(a.CI + bs * (int64_t)(NM * MM), h);
     }
 #pragma unroll
     for (int i = 0; i < NM; i++) c1 += Gr[i][i];
@@ -488,20 +513,22 @@ __device__ __forceinline__ bool pair_body(const QpArgs& a, double* sbuf) {
   const auto kZero = std::integral_constant<int, 0>{};
 
   // ---------------------------------------------------------------- equality phase
-  // Fully unrolled, iq = i at step i.  np (own rows) and ce0[i] were loaded a step ahead, and
-  // each step issues the next step's loads BEFORE its part of the CI copy: vector-memory waits
-  // count in issue order, so consuming them then waits for those loads only, not for the CI
-  // pieces streaming in from HBM behind them (issued the other way round, every step waited
-  // for the previous step's copy part: 43.6k instead of ~20k cycles per wave, profiles/r04_s12).
+  // Fully unrolled, iq = i at step i.  Each step issues its CE loads before its part of the CI
+  // copy: vector-memory waits count in issue order, so consuming them waits only for copy parts
+  // issued kCeAhead steps earlier, not for the pieces streaming in behind them (issued the other
+  // way round, every step waited for the previous step's part: 43.6k instead of ~20k cycles per
+  // wave, profiles/r04_s12).
+  constexpr int kDmaFrom = QPGPU_PAIR_DMA_FROM >= 0 ? (QPGPU_PAIR_DMA_FROM < PX ? QPGPU_PAIR_DMA_FROM : PX - 1)
+                                                   : (PX - 1 - kCeAhead > 0 ? PX - 1 - kCeAhead : 0);
   bool done = !ok_lane;
 #pragma unroll
   for (int i = 0; i < PX; i++) {
-    const double c0 = c0n;
+    const double c0 = c0a[i];
 #pragma unroll
-    for (int k = 0; k < H; k++) nph[k] = npn[k];
-    if (i + 1 < PX) load_ce(i + 1 < PX ? i + 1 : 0);
+    for (int k = 0; k < H; k++) nph[k] = cea[i][k];
+    if (i + kCeAhead < PX) load_ce(i + kCeAhead < PX ? i + kCeAhead : 0);
     __builtin_amdgcn_sched_barrier(0);
-    if (dma) dma_ci_part(i, PX);  // every lane (the copy is per wave)
+    if (dma && i >= kDmaFrom) dma_ci_part(i - kDmaFrom, PX - kDmaFrom);  // every lane (per-wave copy)
     __builtin_amdgcn_sched_barrier(0);
     if (!done) {
       iq = i;
@@ -532,6 +559,7 @@ __device__ __forceinline__ bool pair_body(const QpArgs& a, double* sbuf) {
     pf_ce0.retire();
     pf_ci.retire();
     pf_ci0.retire();
+    if (!dma) pf_cil.retire();
   }
   qp_stamp(a, 2);
   bool ci_ready = false;  // wave-uniform: the LDS copy of CI rows 0..kCiRows-1 is complete

@@ -73,6 +73,11 @@ def test_kernel_name_flags_follow_the_flag_rules():
     assert nm(qpgpu.FLAG_FAST | qpgpu.FLAG_WRITE_FACTOR) == ""
     assert nm(qpgpu.FLAG_FORCE_LANE | qpgpu.FLAG_FORCE_WAVE) == ""
     assert nm(0x8) == ""
+    # the lane-pair family: fast build only, (7, 6, 14) only
+    assert nm(qpgpu.FLAG_FAST | qpgpu.FLAG_FORCE_PAIR) == "qp_pair_fast<N=7,P=6,M=14>"
+    assert nm(qpgpu.FLAG_FORCE_PAIR) == ""
+    assert nm(qpgpu.FLAG_FAST | qpgpu.FLAG_FORCE_PAIR | qpgpu.FLAG_FORCE_LANE) == ""
+    assert qpgpu.LIB.qpgpu_kernel_name_flags(7, 0, 14, qpgpu.FLAG_FAST | qpgpu.FLAG_FORCE_PAIR).decode() == ""
 
 
 def test_no_device_fails_loudly():
