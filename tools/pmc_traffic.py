@@ -23,13 +23,15 @@ import sys
 from collections import defaultdict
 
 
-def per_kernel(d, counter, fast):
-    # bench.py also times the other arithmetic build of the lane kernel (other_arithmetic): only
-    # the kernels of the measured build count
+def per_kernel(d, counter, fast, pair=False):
+    # bench.py also times the other arithmetic build of the lane kernel (other_arithmetic) and
+    # the lane-pair kernel (pair_kernel): only the kernels of the measured build count
     vals = defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             kn = r["Kernel_Name"]
+            if ("qp_pair" in kn) != pair:
+                continue
             if r["Counter_Name"] == counter and "qp_" in kn and ("_fast_" in kn) == fast:
                 vals[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
     return vals
@@ -47,8 +49,9 @@ def main():
                        "motion-generation-using-quadratic-programs_amd", "lib", "libqpgpu.so")
     md5 = hashlib.md5(open(lib, "rb").read()).hexdigest() if os.path.exists(lib) else None
     fast = "fast" in kname
-    fe = per_kernel(fetch_dir, "FETCH_SIZE", fast)
-    wr = per_kernel(write_dir, "WRITE_SIZE", fast)
+    pair = "qp_pair" in kname
+    fe = per_kernel(fetch_dir, "FETCH_SIZE", fast, pair)
+    wr = per_kernel(write_dir, "WRITE_SIZE", fast, pair)
     kernels = {}
     for k in sorted(set(fe) | set(wr)):
         fk = statistics.median(fe[k]) if fe[k] else 0.0
