@@ -51,7 +51,7 @@ for s in $STEPS; do
       for c in C1 C2 mgqp C3; do run bench_$c 600 python bench.py --config $c --no-cpu --no-c4 --steps 20; done
       run bench_C5 600 python bench.py --config C5 --no-cpu --no-c4 --steps 3 --warmup 1 ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c1 -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-c4 --streams 1 ;;
-    profmgqp) run profmgqp 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profmgqp" -o mgqp -- python3 tools/bench_mgqp.py --steps 3 --no-host --no-cpu --no-c4 ;;
+    profmgqp) run profmgqp 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profmgqp" -o mgqp -- python3 tools/bench_mgqp.py --steps 3 --no-host --no-cpu ;;
     benchmgqp) run benchmgqp 600 python tools/bench_mgqp.py ;;
     benchmgqpw) run benchmgqp_wide 600 python tools/bench_mgqp.py --wide ;;
     pmc)
