@@ -493,15 +493,20 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
       zv[r] = z;
     }
   };
+  // r = R^{-1} d for the active set's inequality rows only (i >= p; LoC: a compile-time bound on
+  // iq, here p).  In the active-set loop only those rows' r feed anything — t1 and the
+  // inequalities' multipliers; the equality constraints' multipliers u[0..p) are never read there,
+  // nor output — and r[i] for i >= p does not depend on the rows below, so the reference's
+  // back-substitution stops at row p (x, f, status and the l1 passes are unchanged).
   auto update_r = [&](auto LoC) {
     constexpr int LO = decltype(LoC)::value;
 #pragma unroll
     for (int i = NM - 1; i >= 0; i--) {
-      if (i < LO || i < iq) {
+      if (i >= LO && i >= p && i < iq) {
         double s = 0.0;
 #pragma unroll
         for (int j = i + 1; j < NM; j++)
-          if (j < LO || j < iq) s += Rv[RI::at(i, j)] * rv[j];
+          if (j < iq) s += Rv[RI::at(i, j)] * rv[j];
         rv[i] = ldiv<F>(dv[i] - s, Rv[RI::at(i, i)], fok);
       }
     }
@@ -747,7 +752,10 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
       }
       compute_d();
       update_z(kZero);
-      update_r(kZero);
+      // (no update_r and no u[:i] update here: r and the equality constraints' multipliers u[0..p)
+      // feed nothing — the active-set loop reads u only for the inequalities (t1, the dual step's
+      // drop, the rollback) and x, f never use u — so the reference's back-substitution of every
+      // equality step is skipped; x, f, status and the l1 passes are unchanged)
       double t2 = 0.0;
       const double zz = dot(zv, zv);
       const double znp = dot(zv, npv);
@@ -755,9 +763,6 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
 #pragma unroll
       for (int k = 0; k < NM; k++) xv[k] += t2 * zv[k];
       uv[i < NM + 1 ? i : NM] = t2;
-#pragma unroll
-      for (int k = 0; k < NM; k++)
-        if (k < i) uv[k] -= t2 * rv[k];
       fval += 0.5 * (t2 * t2) * znp;
       Av[i < NM + 1 ? i : NM] = -i - 1;
       if (!add_constraint(kZero)) {
@@ -1113,7 +1118,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
           if (dual || prim) {
 #pragma unroll
             for (int k = 0; k < NM; k++)
-              if (k < IQLO || k < iq) uv[k] -= t * rv[k];
+              if (k >= p && k < iq) uv[k] -= t * rv[k];  // (u[0..p) are never read)
             lput_lo<IQLO>(uv, iq, lsel_lo<IQLO>(uv, iq) + t);
           }
           bool add_fail = false;

@@ -385,11 +385,12 @@ __device__ __forceinline__ bool pair_body(const QpArgs& a, double* sbuf) {
       zh[k] = z;
     }
   };
+  // (in the loop only the inequality rows i >= p of r feed anything: rows below LO = p skipped)
   auto update_r = [&](auto LoC) {
     constexpr int LO = decltype(LoC)::value;
 #pragma unroll
     for (int i = NM - 1; i >= 0; i--) {
-      if (i < LO || i < iq) {
+      if (i >= LO && i < iq) {
         double s = 0.0;
 #pragma unroll
         for (int j = i + 1; j < NM; j++)
@@ -534,7 +535,9 @@ __device__ __forceinline__ bool pair_body(const QpArgs& a, double* sbuf) {
       iq = i;
       compute_d();
       update_z(kZero);
-      update_r(kZero);
+      // (as qp_lane.hip: no update_r and no u[:i] update here: r and the equality constraints' multipliers u[0..p)
+      // feed nothing — the active-set loop reads u only for the inequalities (t1, the dual step's
+      // drop, the rollback) and x, f never use u — so their back-substitution is skipped; x, f, status and the l1 passes are unchanged)
       double t2 = 0.0;
       const double zz = pdot(zh, zh);
       const double znp = pdot(zh, nph);
@@ -543,9 +546,6 @@ __device__ __forceinline__ bool pair_body(const QpArgs& a, double* sbuf) {
 #pragma unroll
       for (int k = 0; k < H; k++) xh[k] += t2 * zh[k];
       uv[i] = t2;
-#pragma unroll
-      for (int k = 0; k < NM; k++)
-        if (k < i) uv[k] -= t2 * rv[k];
       fval += 0.5 * (t2 * t2) * znp;
       Av[i] = -i - 1;
       if (!add_constraint(kZero)) {
@@ -815,7 +815,7 @@ __device__ __forceinline__ bool pair_body(const QpArgs& a, double* sbuf) {
           if (dual || prim) {
 #pragma unroll
             for (int k = 0; k < NM; k++)
-              if (k < IQLO || k < iq) uv[k] -= t * rv[k];
+              if (k >= IQLO && k < iq) uv[k] -= t * rv[k];  // (u[0..p) are never read)
             lput_lo<IQLO>(uv, iq, lsel_lo<IQLO>(uv, iq) + t);
           }
           bool add_fail = false;

@@ -843,8 +843,11 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
   // as the lead's load/multiply unit — its lanes hold row i-1's R entries (loaded while row i is
   // summed) and, once r[i] is known, write the products R[i][j] r[j] (the same single rounding
   // as the reference's `R[i][j] * r[j]`) to LDS; the lead then adds them in j order.  Called by
-  // every lane of the subgroup.
-  auto update_r = [&](int iq) {
+  // every lane of the subgroup.  Rows lo..iq-1 only: the loop passes lo = p — the equality
+  // constraints' rows of r feed only their multipliers u[0..p), which nothing reads (t1, the
+  // dual step's drop and the rollback use the inequalities' u; x and f never use u), and r[i]
+  // for i >= p does not depend on the rows below.
+  auto update_r = [&](int iq, int lo) {
     if constexpr (!GJR && QPGPU_WAVE_URPF) {
       // row i: s = R[i][i+1] r[i+1] + sum_{j >= i+2} R[i][j] r[j] in j order (the reference's
       // order: +0.0 first, then each product).  r[i+1] stays in a register (no LDS round trip on
@@ -854,7 +857,7 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
       // past the row are read (in-bounds LDS, any value) and their products replaced by +0.0:
       // s is never -0.0 (it starts at +0.0 and a sum is -0.0 only from two -0.0 operands), so
       // adding +0.0 leaves it unchanged.
-      if (lead && iq > 0) {
+      if (lead && iq > lo) {
         constexpr int U = QPGPU_WAVE_URU;
         auto rowp = [&](int i) -> const double* {
           return kPackedR ? Rm + (i * n - (i * (i - 1)) / 2 - i) : Rm + i * JS;
@@ -933,12 +936,12 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
           rn = r;
         };
         int i = iq - 2;
-        for (; i >= 0 && iq - i - 2 < U; i--) row(i, std::false_type{});
-        for (; i >= 0; i--) row(i, std::true_type{});
+        for (; i >= lo && iq - i - 2 < U; i--) row(i, std::false_type{});
+        for (; i >= lo; i--) row(i, std::true_type{});
       }
     } else if constexpr (!GJR) {
       if (lead)
-        for (int i = iq - 1; i >= 0; i--) {
+        for (int i = iq - 1; i >= lo; i--) {
           // row i of R as a pointer (Ri[j] = R[i][j], j >= i): packed rows are contiguous too
           const double* Ri = kPackedR ? Rm + (i * n - (i * (i - 1)) / 2 - i) : Rm + i * JS;
           const double s = seq_fma_up<kUL>(0.0, i + 1, iq, [&](int j) { return Ri[j]; },
@@ -969,11 +972,11 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
           };
 #pragma unroll
           for (int k = 0; k < kRD; k++) fetch_row(iq - 1 - k, ring[k], rd[k], rg[k]);
-          for (int i0 = iq - 1; i0 >= 0; i0 -= kRD) {
+          for (int i0 = iq - 1; i0 >= lo; i0 -= kRD) {
 #pragma unroll
             for (int k = 0; k < kRD; k++) {
               const int i = i0 - k;
-              if (i < 0) break;
+              if (i < lo) break;
               double rc[PU];
 #pragma unroll
               for (int u = 0; u < PU; u++) rc[u] = ring[k][u];
@@ -1006,7 +1009,7 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
         }
       };
       fetch(iq - 1);
-      for (int i = iq - 1; i >= 0; i--) {
+      for (int i = iq - 1; i >= lo; i--) {
 #pragma unroll
         for (int u = 0; u < PU; u++) rc[u] = rn[u];
         fetch(i - 1);  // in flight while row i is finished
@@ -1433,7 +1436,8 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
       const uint64_t e0 = clk();
       compute_d_z(ctl->iq);
       const uint64_t e1 = clk();
-      update_r(ctl->iq);
+      // (no update_r and no u[:iq] update in the equality phase: r and the equality constraints'
+      // multipliers feed nothing, see update_r)
       const uint64_t e2 = clk();
       teq[0] += e1 - e0;
       teq[1] += e2 - e1;
@@ -1451,7 +1455,6 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
       {
         const double t2 = ctl->t2;
         for (int k = ls; k < n; k += S) xv[k] += t2 * zv[k];
-        for (int k = ls; k < ctl->iq; k += S) uv[k] -= t2 * rv[k];
       }
       const uint64_t e3 = clk();
       teq[2] += e3 - e2;
@@ -1714,7 +1717,7 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
       tdet[1] += 1;
       tdet[2] += ctl->iq;
     }
-    update_r(ctl->iq);
+    update_r(ctl->iq, p);
     if (QPGPU_WAVE_STAMPS_DETAIL == 1) tdet[0] += clk() - t1c;
     // t1 = min over active inequalities with r > 0 of u/r (first index on ties), l its constraint
     [[maybe_unused]] double t1best = inf;
@@ -1780,7 +1783,7 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
     kind = ctl->qq;
     if (kind >= 2) {
       const double t = ctl->t;
-      for (int k = ls; k < ctl->iq; k += S) uv[k] -= t * rv[k];
+      for (int k = p + ls; k < ctl->iq; k += S) uv[k] -= t * rv[k];  // (u[0..p) are never read)
       grp_sync<S>();
     }
     t0 = clk();
