@@ -193,9 +193,13 @@ __global__ void __launch_bounds__(kGenBS) qp_generic_kernel(const QpArgs a, doub
       zv[r] = seq_fma_up<kGU>(0.0, iq, n, [&](int j) { return J_(r, j); }, [&](int j) { return dv[j]; });
     __syncthreads();
   };
-  auto update_r = [&](int iq) {  // r = R[:iq, :iq]^{-1} d[:iq] (lead)
+  // r = R[p:iq, p:iq]^{-1} d[p:iq] (lead): the inequality rows only — the equality constraints'
+  // rows feed only their multipliers u[0..p), which nothing reads (t1, the dual step's drop and
+  // the rollback use the inequalities' u; x and f never use u), and r[i] for i >= p does not
+  // depend on the rows below.  For the same reason the equality phase runs none.
+  auto update_r = [&](int iq) {
     if (lead)
-      for (int i = iq - 1; i >= 0; i--) {
+      for (int i = iq - 1; i >= p; i--) {
         const double s = seq_fma_up<kGU>(0.0, i + 1, iq, [&](int j) { return R_(i, j); },
                                          [&](int j) { return rv[j]; });
         rv[i] = (dv[i] - s) / R_(i, i);
@@ -394,13 +398,11 @@ __global__ void __launch_bounds__(kGenBS) qp_generic_kernel(const QpArgs a, doub
       const int iq = c.iq;
       compute_d();
       update_z(iq);
-      update_r(iq);
       if (lead) {
         double t2 = 0.0;
         if (fabs(dot(zv, zv)) > kEps) t2 = (-dot(npv, xv) - EL(ce0b, i)) / dot(zv, npv);
         c.t2 = t2;
         uv[iq] = t2;
-        for (int k = 0; k < iq; k++) uv[k] -= t2 * rv[k];
         c.f += 0.5 * (t2 * t2) * dot(zv, npv);
         Av[i] = -i - 1;
       }
@@ -533,13 +535,13 @@ __global__ void __launch_bounds__(kGenBS) qp_generic_kernel(const QpArgs a, doub
         c.f = inf;
         c.phase = G_DONE;
       } else if (t2 >= inf) {  // dual step
-        for (int k = 0; k < iq; k++) uv[k] -= t * rv[k];
+        for (int k = p; k < iq; k++) uv[k] -= t * rv[k];
         uv[iq] += t;
         iai[l] = l;
         c.ok = 2;
       } else {  // primal and dual step
         c.f += t * dot(zv, npv) * (0.5 * t + uv[iq]);
-        for (int k = 0; k < iq; k++) uv[k] -= t * rv[k];
+        for (int k = p; k < iq; k++) uv[k] -= t * rv[k];
         uv[iq] += t;
         c.ok = fabs(t - t2) < kEps ? 3 : 4;
       }

@@ -311,11 +311,15 @@ __global__ void __launch_bounds__(64) qp_small_kernel(const QpArgs a) {
       for (int i = 0; i < NM; i++) zv[i] = (i < n) ? zb[i] : 0.0;
       sg_sync();
     };
-    // update_r: r = R[:iq,:iq]^{-1} d[:iq], back substitution (replicated)
-    auto update_r = [&]() {
+    // update_r: r = R[lo:iq, lo:iq]^{-1} d[lo:iq], back substitution (replicated).  Only the
+    // inequality rows (lo = p) are computed: the equality constraints' rows feed only their
+    // multipliers u[0..p), which nothing reads (t1, the dual step's drop and the rollback use the
+    // inequalities' u; x and f never use u), and r[i] for i >= p does not depend on the rows
+    // below.  For the same reason the equality phase runs none.
+    auto update_r = [&](int lo) {
 #pragma unroll
       for (int i = NM - 1; i >= 0; i--) {
-        if (i < iq) {
+        if (i >= lo && i < iq) {
           double s = 0.0;
 #pragma unroll
           for (int j = i + 1; j < NM; j++)
@@ -454,7 +458,6 @@ __global__ void __launch_bounds__(64) qp_small_kernel(const QpArgs a) {
       }
       compute_d();
       update_z();
-      update_r();
       double t2 = 0.0;
       const double zz = dot(zv, zv);
       const double znp = dot(zv, npv);
@@ -462,9 +465,6 @@ __global__ void __launch_bounds__(64) qp_small_kernel(const QpArgs a) {
 #pragma unroll
       for (int k = 0; k < NM; k++) xv[k] += t2 * zv[k];
       put<NM + 1>(uv, iq, t2);
-#pragma unroll
-      for (int k = 0; k < NM; k++)
-        if (k < iq) uv[k] -= t2 * rv[k];
       fval += 0.5 * (t2 * t2) * znp;
       put<NM + 1>(Av, i, -i - 1);
       if (!add_constraint()) {
@@ -574,7 +574,7 @@ __global__ void __launch_bounds__(64) qp_small_kernel(const QpArgs a) {
         }
         compute_d();
         update_z();
-        update_r();
+        update_r(p);
         int l = 0;
         double t1 = inf;
 #pragma unroll
@@ -603,7 +603,7 @@ __global__ void __launch_bounds__(64) qp_small_kernel(const QpArgs a) {
         if (t2 >= inf) {  // dual step only
 #pragma unroll
           for (int k = 0; k < NM; k++)
-            if (k < iq) uv[k] -= t * rv[k];
+            if (k >= p && k < iq) uv[k] -= t * rv[k];
           put<NM + 1>(uv, iq, sel<NM + 1>(uv, iq) + t);
           act &= ~(1ull << l);
           delete_constraint(l);
@@ -616,7 +616,7 @@ __global__ void __launch_bounds__(64) qp_small_kernel(const QpArgs a) {
         fval += t * znp * (0.5 * t + sel<NM + 1>(uv, iq));
 #pragma unroll
         for (int k = 0; k < NM; k++)
-          if (k < iq) uv[k] -= t * rv[k];
+          if (k >= p && k < iq) uv[k] -= t * rv[k];
         put<NM + 1>(uv, iq, sel<NM + 1>(uv, iq) + t);
         if (fabs(t - t2) < kEps) {  // full step
           if (!add_constraint()) {
