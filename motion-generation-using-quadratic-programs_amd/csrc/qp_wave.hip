@@ -1081,9 +1081,46 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
   //  3. every lane applies the rotations to its rows of J in order; the lead finishes with
   //     R[:iq, iq-1] = d and the degeneracy test.  Returns through ctl->fin (1 = added).
   static_assert(S >= NMAX, "one lane per rotation");
+  // Fast build, LDS variants: the |h| chain from one prefix sum of squares over the subgroup.
+  // Without a skipped step, distance(a, b) = sqrt(a^2 + b^2) and the carried value is the previous
+  // h, so h_g^2 = d[n-1]^2 + sum_{k<=g} d[n-2-k]^2: lane g takes its square, an inclusive scan
+  // over the subgroup (log2 S shuffles) gives every h at once instead of n-1-iq dependent
+  // hypots on the lead (the largest serial chain left in the equality phase: 25-28k of the mgqp
+  // level's 110k cycles per wave, profiles/r04_s26).  h grows with g, so a step can be skipped
+  // (|h| < eps) only if the first one is: that case and squares outside the fast forms' range
+  // take the serial chain.  Within north_star's 1e-10 like the rest of the fast build.
+  auto h_prefix = [&](int iq) -> bool {
+    if constexpr (F && !GJR && S <= 64) {
+      const int ng = iq < n - 1 ? n - 1 - iq : 0;
+      const int g = ls;
+      const double ag = g < ng ? dv[n - 2 - g] : 0.0;
+      double v = ag * ag;
+#pragma unroll
+      for (int o = 1; o < S; o <<= 1) {
+        const double t = __shfl_up(v, o, S);
+        v += ls >= o ? t : 0.0;
+      }
+      const double d0 = ng > 0 ? dv[n - 1] : 0.0;
+      const double P = __builtin_fma(d0, d0, v);
+      const bool bad = g < ng && (!(P >= 0x1p-600 && P <= 0x1p600) || (g == 0 && P < 4.0 * kEps * kEps));
+      const uint64_t bm = __builtin_amdgcn_ballot_w64(bad);
+      const int sgb = (S >= 64) ? 0 : (int)(threadIdx.x & 63) & ~(S - 1);
+      const uint64_t sgm = (S >= 64) ? ~0ull : ((1ull << (S & 63)) - 1) << sgb;
+      if (bm & sgm) return false;  // this QP's lanes take the serial chain
+      if (g < ng) {
+        GX_(g) = sqrt(P);
+        GF_(g) = 1.0;
+      }
+      if (lead) ctl->ngiv = ng;
+      return true;
+    } else {
+      return false;
+    }
+  };
   auto add_constraint = [&]() {
     const uint64_t h0 = clk();
-    if (lead) {
+    const bool hp = h_prefix(ctl->iq);
+    if (lead && !hp) {
       const int iq = ctl->iq;
       int ng = 0;
       if (QPGPU_WAVE_HCHAIN2 && iq < n) {

@@ -27,7 +27,7 @@ fn.argtypes = [ctypes.c_void_p]
 for rep in range(2):
     st.zero_()
     fn(ctypes.c_void_p(st.data_ptr()))
-    db.solve(family="wave")
+    db.solve(family="wave", fast=os.environ.get("WFAST") == "1")  # WFAST=1: the fast build
     torch.cuda.synchronize()
 fn(None)
 s = st.cpu().numpy().reshape(blocks, 18).astype(np.int64)
