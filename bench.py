@@ -66,10 +66,11 @@ CONFIGS = {
 def arithmetic_of(kname):
     """The arithmetic contract of the kernel that actually ran (qpgpu_kernel_name_flags)."""
     if "fast" in kname:
-        return "fast: fused multiply-adds, shared reciprocals; x, f within 1e-10 relative"
+        return ("fast (opt-in): fused multiply-adds, shared reciprocals; x within 1e-10 relative, "
+                "f within 1e-10 of its terms (not north_star's plain f bar, DESIGN 3.3)")
     if "qp_panel" in kname:
         return ("tolerance: MFMA panel setup + tree-summed loop sums (n > 64 default); x, f within "
-                "1e-10 relative")
+                "1e-10 relative per QP (cpu_baseline.parity)")
     return "exact: the reference's operation order, bitwise"
 
 
@@ -91,7 +92,7 @@ def parse(argv=None):
                     help="workload (default: C1 on one GPU, C4 on N > 1)")
     ap.add_argument("--batch", type=int, default=0, help="QPs per GPU (default: the config's)")
     ap.add_argument("--seed", type=int, default=2026)
-    ap.add_argument("--family", default=None, choices=["lane", "subgroup", "wave", "generic", "pair"],
+    ap.add_argument("--family", default=None, choices=["lane", "subgroup", "wave", "generic"],
                     help="force a kernel family (default: the dispatcher's choice)")
     ap.add_argument("--layout", default="qp_major", choices=["qp_major", "tiled64"],
                     help="batch layout of the resident inputs (include/qpgpu.h)")
@@ -108,11 +109,11 @@ def parse(argv=None):
     ap.add_argument("--kernel-reps", type=int, default=20,
                     help="serialized launches timed for the roofline's kernel duration")
     ap.add_argument("--exact", action="store_true",
-                    help="the bitwise build of the lane kernel (the reference's operation order) "
-                         "instead of QPGPU_FLAG_FAST; the line reports the other one beside it")
+                    help="the bitwise builds (the reference's operation order; the default)")
     ap.add_argument("--fast", action="store_true",
-                    help="QPGPU_FLAG_FAST (the default): the lane kernel's fast build, x and f "
-                         "within north_star's 1e-10 of the reference with the same decisions")
+                    help="QPGPU_FLAG_FAST instead: fused multiply-adds and shared reciprocals — x "
+                         "within 1e-10 of the reference, f only relative to its terms (DESIGN "
+                         "3.3); the default line reports it beside the bitwise build")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c4", action="store_true", help="skip the N = 1 line's C4-on-one-GPU record")
@@ -123,7 +124,6 @@ def parse(argv=None):
         args.gather = "none"
     if args.exact and args.fast:
         ap.error("--exact and --fast exclude each other")
-    args.fast = not args.exact
     return args
 
 
@@ -150,12 +150,67 @@ def cpu_chunk(pr):
     return max(1, min(pr.batch, 8192, 8192 * 1792 // bpq))
 
 
-def cpu_baseline(pr, seconds, gpu_out=None):
-    """The oracle (CPU restatement, -O2, 1 thread) on the same resident batch, repeated until
-    `seconds` of wall time: a bounded sample of the same workload.  Its first chunk is also the
-    parity sample: the GPU's x / f / status for those QPs against the oracle's (gpu_out)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+# QPs the parity check covers: the whole batch, except C5 (4 096 QPs of ~134 l1 passes: ~26 s of
+# oracle time on 16 threads), where it takes the first PARITY_QPS_C5 QPs
+PARITY_QPS_C5 = 256
+TOL = 1e-10  # north_star: "within 1e-10 relative"
+
+
+def parity_qps(pr):
+    return pr.batch if pr.n <= 64 else min(pr.batch, PARITY_QPS_C5)
+
+
+def parity_record(pr, layout, got, ref, against, ref_on_device=False):
+    """north_star's parity bar per QP over the first len(ref[1]) QPs of `pr`: status identical,
+    ||x - x_ref||_inf / ||x_ref||_inf <= 1e-10 and |f - f_ref| / |f_ref| <= 1e-10 (the plain
+    relative error — the gate), plus the bitwise flags and, as an extra figure only, f relative to
+    its terms max(|f_ref|, 0.5|x'Gx| + |g0'x|)."""
     import numpy as np
+    import qpgpu
+
+    n = pr.n
+    B = len(ref[1])
+    xg = np.asarray(got[0]).reshape(-1)
+    if layout == "tiled64":
+        xg = qpgpu.from_tiled64(xg, pr.batch, (n,))
+    xg = xg.reshape(-1, n)[:B]
+    fg, sg = np.asarray(got[1])[:B], np.asarray(got[2])[:B]
+    xo = np.asarray(ref[0]).reshape(-1)
+    if ref_on_device and layout == "tiled64":  # the other build's device output, same layout
+        xo = qpgpu.from_tiled64(xo, pr.batch, (n,))
+    xo = xo.reshape(-1, n)[:B]
+    fo, so = np.asarray(ref[1])[:B], np.asarray(ref[2])[:B]
+    ok = (so == qpgpu.QP_OK) & (sg == so)
+    exq, efq = qpgpu.rel_error_per_qp(xg[ok], xo[ok], fg[ok], fo[ok])
+    sc = qpgpu.objective_term_scale(pr.G[:B][ok], pr.g0[:B][ok], xo[ok])
+    _, efs = qpgpu.rel_error_per_qp(xg[ok], xo[ok], fg[ok], fo[ok], f_scale=sc)
+    mx = lambda a: float(a.max()) if a.size else 0.0
+    bits = lambda a, b: bool(np.array_equal(np.ascontiguousarray(a).view(np.uint64),
+                                            np.ascontiguousarray(b).view(np.uint64)))
+    nx, nf = int((exq > TOL).sum()), int((efq > TOL).sum())
+    status_equal = int((sg == so).sum())
+    worst = int(np.flatnonzero(ok)[int(np.argmax(efq))]) if efq.size else None
+    return {"qps": int(B), "status_equal": status_equal, "qps_ok": int(ok.sum()),
+            "x_bitwise_equal": bits(xg[ok], xo[ok]), "f_bitwise_equal": bits(fg[ok], fo[ok]),
+            "max_rel_err_x": mx(exq), "max_rel_err_f": mx(efq),
+            "qps_rel_err_x_above_tol": nx, "qps_rel_err_f_above_tol": nf,
+            "meets_north_star": bool(status_equal == B and nx == 0 and nf == 0),
+            "worst_f_qp": worst,
+            "max_rel_err_f_vs_terms": mx(efs),
+            "max_f_cancellation": mx(sc / np.maximum(np.abs(fo[ok]), np.finfo(np.float64).tiny)),
+            "rel_err_definition": ("gate, per QP: ||x-x_ref||_inf/||x_ref||_inf <= 1e-10 and "
+                                   "|f-f_ref|/|f_ref| <= 1e-10 (status identical); extra: "
+                                   "|f-f_ref|/max(|f_ref|, 0.5|x'Gx|+|g0'x|) and the largest "
+                                   "cancellation factor terms/|f|"),
+            "tolerance": TOL, "against": against}
+
+
+def cpu_baseline(pr, seconds, layout, gpu_out=None):
+    """The oracle (CPU restatement, -O2) on the same resident batch: 1 thread repeated until
+    `seconds` of wall time on a bounded chunk, then CPU_THREAD_CAP threads over the batch.  The
+    parity check runs the oracle once over the whole batch (parity_qps) on the capped threads and
+    compares the GPU's x / f / status of the same QPs (gpu_out) per QP."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
 
     oracle.lib()
@@ -163,47 +218,20 @@ def cpu_baseline(pr, seconds, gpu_out=None):
     chunk = cpu_chunk(pr)
     sub = pr.slice(0, chunk)
     done = 0
-    parity = None
     t0 = time.perf_counter()
     while True:
-        xo, fo, so, _ = oracle.solve_batch(sub, max_steps=cap, threads=1)
+        oracle.solve_batch(sub, max_steps=cap, threads=1)
         done += chunk
         el = time.perf_counter() - t0
-        if parity is None and gpu_out is not None:
-            xg, fg, sg = (a[:chunk] for a in gpu_out)
-            ok = so == 0
-            def absrel(a, b):
-                d = np.abs(a - b) / np.maximum(1.0, np.abs(b))
-                return float(d.max()) if d.size else 0.0
-            # north_star's criterion, per QP: ||x - x_ref||_inf / ||x_ref||_inf; |f - f_ref| / |f_ref|
-            # plainly and relative to the objective's terms max(|f_ref|, 0.5|x'Gx| + |g0'x|)
-            import qpgpu
-            sc = qpgpu.objective_term_scale(sub.G[ok], sub.g0[ok], xo[ok])
-            exq, efq = qpgpu.rel_error_per_qp(xg[ok], xo[ok], fg[ok], fo[ok])
-            _, efs = qpgpu.rel_error_per_qp(xg[ok], xo[ok], fg[ok], fo[ok], f_scale=sc)
-            canc = sc / np.maximum(np.abs(fo[ok]), np.finfo(np.float64).tiny) if ok.any() else np.zeros(0)
-            mx = lambda a: float(a.max()) if a.size else 0.0
-            parity = {"qps": int(chunk), "status_equal": int((sg == so).sum()),
-                      "x_bitwise_equal": bool(np.array_equal(xg[ok].view(np.uint64), xo[ok].view(np.uint64))),
-                      "f_bitwise_equal": bool(np.array_equal(fg[ok].view(np.uint64), fo[ok].view(np.uint64))),
-                      "max_rel_err_x": mx(exq), "max_rel_err_f": mx(efq),
-                      "max_rel_err_f_vs_terms": mx(efs),
-                      "qps_rel_err_f_above_tol": int((efq > 1e-10).sum()),
-                      "max_f_cancellation": mx(canc),
-                      "rel_err_definition": ("per QP: ||x-x_ref||_inf/||x_ref||_inf; |f-f_ref|/|f_ref|; and "
-                                             "|f-f_ref|/max(|f_ref|, 0.5|x'Gx|+|g0'x|) (f's terms may cancel: "
-                                             "max_f_cancellation = terms / |f|)"),
-                      "max_abs_or_rel_err_x": absrel(xg[ok], xo[ok]),
-                      "max_abs_or_rel_err_f": absrel(fg[ok], fo[ok]),
-                      "tolerance": 1e-10, "checker": "oracle/qp_oracle.c on the same QPs"}
         if el >= seconds:
             break
     out = {"value": done / el, "unit": "QP solves/s", "cores": 1, "kind": "port",
            "sample": f"oracle/qp_oracle.c (-O2, 1 thread) re-solving the first {chunk} QPs of the "
                      f"same synthetic batch {done // chunk}x ({done} solves, {el:.1f} s)"}
     # the same restatement on the host's cores, one std::thread per core
-    # over contiguous shards — capped at the CPU share a one-GPU box grants this job (16 threads;
-    # os.cpu_count() reports the whole machine, which this job may not use)
+    # over contiguous shards — capped at the CPU share a one-GPU box grants this job: the pool's
+    # rule is 16 worker threads per GPU job (os.cpu_count() reports the whole machine, most of
+    # which belongs to other jobs), so 16 is "all cores" this job may use
     threads = max(1, min(CPU_THREAD_CAP, os.cpu_count() or 1))
     big = pr.slice(0, min(pr.batch, chunk * threads * 4))
     done_mt = 0
@@ -221,13 +249,23 @@ def cpu_baseline(pr, seconds, gpu_out=None):
     except OSError:
         pass
     out["multi_thread"] = {"value": done_mt / el_mt, "threads": threads, "nproc": os.cpu_count(),
-                           "thread_cap": f"{CPU_THREAD_CAP} = the CPU share of a one-GPU job on the box; "
-                                         f"nproc counts the whole machine", "cpu_model": model,
+                           "per_thread": done_mt / el_mt / threads,
+                           "thread_cap": f"{CPU_THREAD_CAP} = the worker-thread share the GPU pool grants a "
+                                         f"one-GPU job; nproc counts the whole machine",
+                           "cpu_model": model,
                            "sample": f"{big.batch} QPs per pass, {done_mt // big.batch} passes, "
                                      f"{el_mt:.1f} s"}
     out["cpu_model"] = model
-    if parity is not None:
-        out["parity"] = parity
+    if gpu_out is not None:
+        P = parity_qps(pr)
+        t0 = time.perf_counter()
+        xo, fo, so, _ = oracle.solve_batch(pr.slice(0, P), max_steps=cap, threads=threads)
+        rec = parity_record(pr, layout, gpu_out, (xo, fo, so),
+                            f"oracle/qp_oracle.c on the same QPs ({threads} threads, "
+                            f"{time.perf_counter() - t0:.2f} s)")
+        if P < pr.batch:
+            rec["sample"] = f"the first {P} of {pr.batch} QPs (C5: ~134 l1 passes per QP)"
+        out["parity"] = rec
     return out
 
 
@@ -450,54 +488,16 @@ def main():
         torch.cuda.synchronize(dev)
         theirs = [t.clone() for t in outs[0]]
         # the exact (bitwise) build's output is the reference of the comparison, whichever
-        # build this line measures
+        # build this line measures (cpu_baseline.parity checks the line's own build against the
+        # oracle over the whole batch); every QP of the batch, plain and terms-relative f
         ex_, fa_ = (theirs, mine) if args.fast else (mine, theirs)
-        ok_ = (ex_[2] == qpgpu.QP_OK).cpu().numpy()
-        efs = None
-        if args.layout == "qp_major":
-            xr_ = ex_[0].reshape(B, -1).cpu().numpy()[ok_]
-            exq, efq = qpgpu.rel_error_per_qp(fa_[0].reshape(B, -1).cpu().numpy()[ok_], xr_,
-                                              fa_[1].cpu().numpy()[ok_], ex_[1].cpu().numpy()[ok_])
-            sc = qpgpu.objective_term_scale(pr.G[ok_], pr.g0[ok_], xr_)
-            _, efs = qpgpu.rel_error_per_qp(fa_[0].reshape(B, -1).cpu().numpy()[ok_], xr_,
-                                            fa_[1].cpu().numpy()[ok_], ex_[1].cpu().numpy()[ok_], f_scale=sc)
-        else:
-            exq, efq = None, qpgpu.rel_error_per_qp(np.zeros((int(ok_.sum()), 0)), np.zeros((int(ok_.sum()), 0)),
-                                                    fa_[1].cpu().numpy()[ok_], ex_[1].cpu().numpy()[ok_])[1]
         other = {"arithmetic": arithmetic_of(kname_other), "kernel": kname_other,
                  "kernel_ms": ko, "frac": bpq * B / (ko * 1e-3) / 1e9 / HBM_PEAK_GBS,
                  "status_identical": bool(torch.equal(mine[2], theirs[2])),
-                 "max_rel_x": (float(exq.max()) if exq is not None and exq.size else None),
-                 "max_rel_f": float(efq.max()) if efq.size else 0.0,
-                 "max_rel_f_vs_terms": (float(efs.max()) if efs is not None and efs.size else None),
-                 "rel_err_of": ("the fast build against the exact build, per QP (||dx||_inf/||x||_inf, "
-                                "|df|/|f|, |df|/max(|f|, 0.5|x'Gx|+|g0'x|))")}
-
-    # the lane-pair kernel (qp_pair.hip: one QP per two lanes, two waves per SIMD),
-    # measured beside the line's kernel on the same box: its kernel time and its agreement with
-    # this line's solve of set 0
-    pair_rec = None
-    kname_pair = qpgpu.LIB.qpgpu_kernel_name_flags(n, p, m, qpgpu.FLAG_FAST | qpgpu.FLAG_FORCE_PAIR).decode()
-    if world == 1 and not args.family and args.fast and kname_pair and args.layout == "qp_major":
-        launcher(0, 0, cs, True, "pair")()  # first launch (code-object load)
-        torch.cuda.synchronize(dev)
-        kp = kernel_ms(True, fast=True, family="pair")
-        launcher(0, 0, cs)()
-        torch.cuda.synchronize(dev)
-        mine = [t.clone() for t in outs[0]]
-        launcher(0, 0, cs, True, "pair")()
-        torch.cuda.synchronize(dev)
-        theirs = [t.clone() for t in outs[0]]
-        ok_ = (mine[2] == qpgpu.QP_OK).cpu().numpy()
-        exq, _ = qpgpu.rel_error_per_qp(theirs[0].reshape(B, -1).cpu().numpy()[ok_],
-                                        mine[0].reshape(B, -1).cpu().numpy()[ok_],
-                                        theirs[1].cpu().numpy()[ok_], mine[1].cpu().numpy()[ok_])
-        pair_rec = {"kernel": kname_pair, "kernel_ms": kp, "frac": bpq * B / (kp * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                    "status_identical": bool(torch.equal(mine[2], theirs[2])),
-                    "max_rel_x_vs_line": float(exq.max()) if exq.size else 0.0,
-                    "note": "one QP per lane pair, 32 QPs per wave, two waves per SIMD; not the "
-                            "default: its duplicated serial chains cost more than the co-resident "
-                            "wave hides (DESIGN 5.9)"}
+                 "fast_vs_exact": parity_record(pr, args.layout, [t.cpu().numpy() for t in fa_],
+                                                [t.cpu().numpy() for t in ex_],
+                                                "the exact build (bitwise to the oracle) on the same QPs",
+                                                ref_on_device=True)}
 
     gather_ms = gat.time_one() if gat else None  # one step's gather alone, same payload
 
@@ -551,12 +551,8 @@ def main():
     hist = torch.bincount(hb.iters[:B].to(torch.int64).clamp(min=0)).cpu().tolist()
     gpu_sample = None
     if world == 1 and not args.no_cpu:
-        # the QPs the CPU baseline's parity sample solves (set 0, QP order)
-        c = cpu_chunk(pr)
-        xs = hb.x.reshape(-1).cpu().numpy()
-        if args.layout == "tiled64":
-            xs = qpgpu.from_tiled64(xs, B, (n,))
-        gpu_sample = (xs.reshape(-1, n)[:c], hb.f[:c].cpu().numpy(), hb.status[:c].cpu().numpy())
+        # set 0's results from that launch (the batch the parity check re-solves on the CPU)
+        gpu_sample = (hb.x.cpu().numpy(), hb.f.cpu().numpy(), hb.status.cpu().numpy())
 
     if dist:
         t = torch.tensor([elapsed, elapsed1, kern_cold, kern_warm, gather_ms or 0.0, kern_cold_pair,
@@ -665,8 +661,6 @@ def main():
     }
     if other:
         out["other_arithmetic"] = other
-    if pair_rec:
-        out["pair_kernel"] = pair_rec
     if gather:
         out["gather_ms"] = gather_ms
         out["gather_bytes_per_rank"] = gat.bytes_per_rank
@@ -681,7 +675,7 @@ def main():
     if c4_one:
         out["c4_one_gpu"] = c4_one
     if world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(pr, args.cpu_seconds, gpu_sample)
+        out["cpu_baseline"] = cpu_baseline(pr, args.cpu_seconds, args.layout, gpu_sample)
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -123,16 +123,13 @@ enum qpgpu_error {
  *             reference's solve_quadprog takes any n, p, m (QuadProg++.hh:69-72).  The default
  *             for the shapes no other family covers (n > 256 or m > 1024); bitwise with the
  *             reference's operation order; ~2 n^2 + 12 n + 2 m doubles of workspace per QP.
- *   PAIR      one QP per pair of lanes, 32 QPs per wave and two waves per SIMD (qp_pair.hip):
- *             only with QPGPU_FLAG_FAST (its pair sums are not the reference's order), only
- *             the QP-major shape (7, 6, 14), not for qpgpu_solve_batched_eq.
- * Forcing a family that does not cover the shape returns QPGPU_ERR_UNSUPPORTED_SHAPE; forcing
- * PAIR without QPGPU_FLAG_FAST is QPGPU_ERR_INVALID_ARGUMENT. */
+ * Forcing a family that does not cover the shape returns QPGPU_ERR_UNSUPPORTED_SHAPE.
+ * (Bit 0x1000 selected a lane-pair kernel in ABI 4's round-4 builds; it measured slower than
+ * LANE and was removed from the library — the bit is now unknown: QPGPU_ERR_INVALID_ARGUMENT.) */
 #define QPGPU_FLAG_FORCE_LANE 0x100u
 #define QPGPU_FLAG_FORCE_SUBGROUP 0x200u
 #define QPGPU_FLAG_FORCE_WAVE 0x400u
 #define QPGPU_FLAG_FORCE_GENERIC 0x800u
-#define QPGPU_FLAG_FORCE_PAIR 0x1000u
 
 typedef struct qpgpu_problem_desc {
   int32_t n;         /* variables                      (G.ncols() in the reference)  */

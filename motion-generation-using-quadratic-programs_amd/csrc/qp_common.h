@@ -311,8 +311,8 @@ __device__ __forceinline__ int64_t qbase(int64_t b, int E) {
   else
     return (b >> 6) * (int64_t)(64 * E) + (b & 63);
 }
-__device__ __forceinline__ int64_t qbase_rt(int64_t b, int E, int T) {
-  return T == 1 ? b * (int64_t)E : (b >> 6) * (int64_t)(64 * E) + (b & 63);
+__device__ __forceinline__ int64_t qbase_rt(int64_t b, int64_t E, int T) {
+  return T == 1 ? b * E : (b >> 6) * (64 * E) + (b & 63);
 }
 
 struct QpArgs {

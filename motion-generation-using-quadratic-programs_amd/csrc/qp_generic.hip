@@ -87,11 +87,11 @@ __global__ void __launch_bounds__(kGenBS) qp_generic_kernel(const QpArgs a, doub
 #define J_(r_, c_) Jm[(int64_t)(c_) * n + (r_)]
 #define R_(i_, j_) Rm[(int64_t)(i_) * n + (j_)]
 #define EL(ptr, e) (ptr)[(int64_t)(e) * T]
-  const double* Gb = a.G + qbase_rt(b, n * n, T);
+  const double* Gb = a.G + qbase_rt(b, (int64_t)n * n, T);
   const double* g0b = a.g0 + qbase_rt(b, n, T);
-  const double* CEb = a.CE + qbase_rt(b, n * p, T);
+  const double* CEb = a.CE + qbase_rt(b, (int64_t)n * p, T);
   const double* ce0b = a.ce0 + qbase_rt(b, p, T);
-  const double* CIb = a.CI + qbase_rt(b, n * m, T);
+  const double* CIb = a.CI + qbase_rt(b, (int64_t)n * m, T);
   const double* ci0b = a.ci0 + qbase_rt(b, m, T);
   const double inf = dinf();
   const int64_t nn = (int64_t)n * n;
@@ -134,7 +134,7 @@ __global__ void __launch_bounds__(kGenBS) qp_generic_kernel(const QpArgs a, doub
     __syncthreads();
   }
   if (a.flags & QPGPU_FLAG_WRITE_FACTOR) {  // G <- the reference's G after the call
-    double* Gw = a.G + qbase_rt(b, n * n, T);
+    double* Gw = a.G + qbase_rt(b, (int64_t)n * n, T);
     for (int64_t e = tid; e < nn; e += kGenBS) EL(Gw, e) = Rm[e];
   }
   const bool chol_ok = c.status == QPGPU_QP_OK;
@@ -393,7 +393,7 @@ __global__ void __launch_bounds__(kGenBS) qp_generic_kernel(const QpArgs a, doub
   // ---------------------------------------------------------------- equality phase
   if (chol_ok) {
     for (int i = 0; i < p; i++) {
-      for (int j = tid; j < n; j += kGenBS) npv[j] = EL(CEb, j * p + i);
+      for (int j = tid; j < n; j += kGenBS) npv[j] = EL(CEb, (int64_t)j * p + i);
       __syncthreads();
       const int iq = c.iq;
       compute_d();
@@ -616,6 +616,7 @@ __global__ void __launch_bounds__(kGenBS) qp_generic_kernel(const QpArgs a, doub
 
 // Largest shape the generic kernel accepts: n*n and the workspace offsets stay within int64 and a
 // QP's workspace within 2^34 doubles (128 GiB); int32 element indices of the inputs (n*n, n*m).
+// CE offsets (n*p, j*p + i) are computed in int64, so p is not bounded here.
 extern "C" int qpk_generic_covers(int n, int m) {
   return n >= 1 && m >= 0 && (int64_t)n * n < ((int64_t)1 << 31) && (int64_t)n * m < ((int64_t)1 << 31);
 }

@@ -98,6 +98,12 @@ constexpr int kScanDepth = 2;
 #ifndef QPGPU_LANE_DMA_P0
 #define QPGPU_LANE_DMA_P0 0
 #endif
+// A/B builds only (tools/ab_build.sh): the fast build's invalid-fast-form exit also at the top of
+// every loop pass (DESIGN §5.6 — why the product build has it after the equality phase only);
+// 2: the same check compiled in but never taken at run time (max_steps is never below -1)
+#ifndef QPGPU_LANE_LOOPTOP_EXIT
+#define QPGPU_LANE_LOOPTOP_EXIT 0
+#endif
 
 // ---- arithmetic of the fast build (frcp, rcp_ok, ldiv_r, ldiv, ldistance): qp_common.h,
 // shared with the lane-pair kernel (qp_pair.hip).
@@ -1019,6 +1025,12 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
     uint64_t tscan = 0, tsel = 0, nloop = 0, tfirst = 0;  // diagnostic stamps only
     [[maybe_unused]] uint64_t tdzr = 0, tstep = 0;        // (QPGPU_LANE_STAMPS == 2: l2a split)
     while (wave_any(active)) {
+      if constexpr (F && QPGPU_LANE_LOOPTOP_EXIT == 1) {
+        if (wave_any(!fok)) return false;
+      }
+      if constexpr (F && QPGPU_LANE_LOOPTOP_EXIT == 2) {
+        if (wave_any(!fok) && a.max_steps < -1) return false;
+      }
       const uint64_t tl0 = (kStamps && a.stamps) ? __builtin_amdgcn_s_memtime() : 0;
       scan_pass();
       const uint64_t tl1 = (kStamps && a.stamps) ? __builtin_amdgcn_s_memtime() : 0;
@@ -1208,6 +1220,13 @@ static void launch_lane_t(const QpArgs& a, hipStream_t stream) {
   if constexpr (NM == 7 && MM == 14 && T == 1)
     if (a.n == NM && a.m == MM && !a.x_eq && a.p == 6)
       hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, 6>), g, blk, 0, stream, a);
+  return;
+#endif
+#ifdef QPGPU_LANE_AB_N8P0ONLY
+  // A/B / ISA-study builds: only the QP-major (8, 0, 16) instantiation
+  if constexpr (NM == 8 && MM == 16 && T == 1)
+    if (a.n == NM && a.m == MM && !a.x_eq && a.p == 0)
+      hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, 0>), g, blk, 0, stream, a);
   return;
 #endif
   if (a.n == NM && a.m == MM && !a.x_eq) {

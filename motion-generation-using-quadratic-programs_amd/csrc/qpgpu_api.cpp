@@ -24,9 +24,6 @@ extern "C" const char* qpk_lane_name(int n, int p, int m);
 extern "C" hipError_t qpk_launch_lane_fast(const qpk::QpArgs* a, hipStream_t stream, int* handled,
                                            const char** name);
 extern "C" const char* qpk_lane_name_fast(int n, int p, int m);
-extern "C" hipError_t qpk_launch_pair(const qpk::QpArgs* a, hipStream_t stream, int* handled,
-                                      const char** name);
-extern "C" const char* qpk_pair_name(int n, int p, int m);
 extern "C" hipError_t qpk_launch_medium_ws(const qpk::QpArgs* a, hipStream_t stream, int* handled,
                                            const char** name, double* ws);
 extern "C" int64_t qpk_medium_workspace_bytes(int n, int m, int64_t batch);
@@ -62,11 +59,10 @@ int default_max_steps(int n, int p, int m) { return 1000 + 100 * (n + p + m); }
 // most one forced family.  Shared by validate() and qpgpu_kernel_name_flags().
 bool flags_valid(uint32_t flags) {
   const uint32_t fam = QPGPU_FLAG_FORCE_LANE | QPGPU_FLAG_FORCE_SUBGROUP | QPGPU_FLAG_FORCE_WAVE |
-                       QPGPU_FLAG_FORCE_GENERIC | QPGPU_FLAG_FORCE_PAIR;
+                       QPGPU_FLAG_FORCE_GENERIC;
   const uint32_t known = QPGPU_FLAG_WRITE_FACTOR | QPGPU_FLAG_EXACT | QPGPU_FLAG_FAST | fam;
   if (flags & ~known) return false;
   if ((flags & QPGPU_FLAG_FAST) && (flags & (QPGPU_FLAG_EXACT | QPGPU_FLAG_WRITE_FACTOR))) return false;
-  if ((flags & QPGPU_FLAG_FORCE_PAIR) && !(flags & QPGPU_FLAG_FAST)) return false;  // fast-only family
   const uint32_t f = flags & fam;
   return (f & (f - 1)) == 0;
 }
@@ -155,9 +151,15 @@ int qpgpu_max_m(void) {
 // 2.2 vs 3.5 ms) and at m = 64; the S = 8 subgroup kernel still wins at n <= 8, m <= 32.
 static bool default_small(int n, int m) { return n <= 8 && m <= 32; }
 
+// Largest device workspace one generic-kernel launch uses (bytes); larger batches run as
+// sub-batches (solve_batched_impl).  4 GiB; qpgpu_debug_set_generic_ws_cap lowers it in tests.
+static int64_t g_generic_ws_cap = (int64_t)4 << 30;
+
 const char* qpgpu_kernel_name_flags(int32_t n, int32_t p, int32_t m, uint32_t flags) {
   if (!flags_valid(flags)) return "";  // the launch would be rejected (QPGPU_ERR_INVALID_ARGUMENT)
-  if (flags & QPGPU_FLAG_FORCE_PAIR) return qpk_pair_name(n, p, m) ? qpk_pair_name(n, p, m) : "";
+  // the generic family has no fast build: FAST | FORCE_GENERIC launches the generic kernel
+  // (solve_batched_impl), so it is named before the fast builds
+  if (flags & QPGPU_FLAG_FORCE_GENERIC) return qpk_generic_name(n, p, m) ? qpk_generic_name(n, p, m) : "";
   if ((flags & QPGPU_FLAG_FAST) && n > 0 && p >= 0 && m >= 0) {
     // the fast builds: the lane kernel's where it covers the shape, else the wave kernel's LDS
     // variants (n <= 64, m <= 256); a forced family keeps to that family
@@ -267,19 +269,50 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
     e = qpk_launch_medium_ws(&a, s, &handled, nullptr, ws);
     return QPGPU_SUCCESS;
   };
+  // The generic kernel's workspace is per QP (2n^2 + 12n + 2m doubles): a large shape launches
+  // over sub-batches whose workspace stays within g_generic_ws_cap (one allocation reused by every
+  // sub-batch in stream order), instead of one allocation for the whole batch — n = 2000 over
+  // 1000 QPs would otherwise ask for ~64 GB and keep it cached.  TILED64 sub-batches are whole
+  // 64-QP tiles, so each one's arrays start at a tile boundary.
   auto launch_generic = [&]() -> int {
     if (!qpk_generic_covers(a.n, a.m)) return QPGPU_SUCCESS;  // handled stays 0
+    const int64_t per = qpk_generic_workspace_bytes(a.n, a.m, 1);
+    int64_t chunk = a.batch;
+    if (per * a.batch > g_generic_ws_cap) {
+      chunk = g_generic_ws_cap / per;
+      if (a.tile == 64) chunk = chunk / 64 * 64;
+      if (chunk < (a.tile == 64 ? 64 : 1)) chunk = a.tile == 64 ? 64 : 1;
+    }
     double* ws = nullptr;
-    const int wrc = device_workspace(qpk_generic_workspace_bytes(a.n, a.m, a.batch), s, &ws);
+    const int wrc = device_workspace(per * (chunk < a.batch ? chunk : a.batch), s, &ws);
     if (wrc) return wrc;
     handled = 1;
-    e = qpk_launch_generic(&a, s, ws);
+    const int64_t n = a.n, p = a.p, m = a.m;
+    auto off = [&](int64_t b0, int64_t E) { return a.tile == 64 ? (b0 / 64) * 64 * E : b0 * E; };
+    for (int64_t b0 = 0; b0 < a.batch; b0 += chunk) {
+      qpk::QpArgs c = a;
+      c.batch = (a.batch - b0 < chunk) ? a.batch - b0 : chunk;
+      c.G = a.G + off(b0, n * n);
+      c.g0 = a.g0 + off(b0, n);
+      if (a.CE) c.CE = a.CE + off(b0, n * p);
+      if (a.ce0) c.ce0 = a.ce0 + off(b0, p);
+      if (a.CI) c.CI = a.CI + off(b0, n * m);
+      if (a.ci0) c.ci0 = a.ci0 + off(b0, m);
+      c.x = a.x + off(b0, n);
+      c.f = a.f + b0;
+      c.status = a.status + b0;
+      if (a.iters) c.iters = a.iters + b0;
+      if (a.x_eq) c.x_eq = a.x_eq + off(b0, n);
+      if (a.f_eq) c.f_eq = a.f_eq + b0;
+      if (a.st_eq) c.st_eq = a.st_eq + b0;
+      c.stamps = nullptr;
+      e = qpk_launch_generic(&c, s, ws);
+      if (e != hipSuccess) break;
+    }
     return QPGPU_SUCCESS;
   };
   int wrc = QPGPU_SUCCESS;
-  if (d->flags & QPGPU_FLAG_FORCE_PAIR) {
-    e = qpk_launch_pair(&a, s, &handled, nullptr);
-  } else if (d->flags & QPGPU_FLAG_FORCE_GENERIC) {
+  if (d->flags & QPGPU_FLAG_FORCE_GENERIC) {
     wrc = launch_generic();
   } else if (d->flags & QPGPU_FLAG_FORCE_LANE) {
     e = launch_lane();
@@ -305,7 +338,6 @@ static bool family_covers(uint32_t flags, int n, int p, int m) {
   if (flags & QPGPU_FLAG_FORCE_SUBGROUP) return qpk_small_name(n, p, m) != nullptr;
   if (flags & QPGPU_FLAG_FORCE_WAVE) return qpk_medium_name(n, p, m) != nullptr;
   if (flags & QPGPU_FLAG_FORCE_GENERIC) return qpk_generic_covers(n, m) != 0;
-  if (flags & QPGPU_FLAG_FORCE_PAIR) return qpk_pair_name(n, p, m) != nullptr;
   return qpgpu_kernel_name(n, p, m)[0] != 0;
 }
 
@@ -458,6 +490,10 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const doubl
 // Diagnostic hook (not in include/qpgpu.h): device buffer of kStampSlots uint64 per wave that
 // the next launches fill with s_memtime phase stamps; NULL turns it off.
 void qpgpu_debug_set_stamps(void* dev_buf) { g_stamps = static_cast<uint64_t*>(dev_buf); }
+
+// Test hook (not in include/qpgpu.h): the generic kernel's per-launch workspace cap in bytes
+// (<= 0 restores the 4 GiB default), so the sub-batch path runs on small shapes.
+void qpgpu_debug_set_generic_ws_cap(int64_t bytes) { g_generic_ws_cap = bytes > 0 ? bytes : ((int64_t)4 << 30); }
 
 int qpgpu_relayout(int64_t batch, int32_t elems, const double* src, double* dst, int32_t to_tiled,
                    void* stream) {

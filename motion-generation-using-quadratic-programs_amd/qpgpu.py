@@ -50,10 +50,8 @@ FLAG_FORCE_LANE = 0x100
 FLAG_FORCE_SUBGROUP = 0x200
 FLAG_FORCE_WAVE = 0x400
 FLAG_FORCE_GENERIC = 0x800  # any shape: the generic workspace kernel (qp_generic.hip)
-FLAG_FORCE_PAIR = 0x1000  # one QP per lane pair (qp_pair.hip): FAST only, (7,6,14)
 FAMILY_FLAGS = {None: 0, "auto": 0, "lane": FLAG_FORCE_LANE, "subgroup": FLAG_FORCE_SUBGROUP,
-                "wave": FLAG_FORCE_WAVE, "generic": FLAG_FORCE_GENERIC,
-                "pair": FLAG_FORCE_PAIR}
+                "wave": FLAG_FORCE_WAVE, "generic": FLAG_FORCE_GENERIC}
 LAYOUT_QP_MAJOR = 0
 LAYOUT_TILED64 = 1
 LAYOUTS = {None: 0, "qp_major": LAYOUT_QP_MAJOR, "tiled64": LAYOUT_TILED64}

@@ -1,11 +1,15 @@
 """GPU parity: the gfx950 kernels (through the C-ABI) against the oracle on identical inputs.
 
-Bar: per-QP status and iteration count identical, x and f BITWISE identical (the kernels keep
-the reference's operation order; north_star's stated tolerance is 1e-10 relative, and a
-failure message reports the worst relative error so a near-miss is visible).  The one exception
-is the default n > 64 path, whose setup runs as blocked f64 MFMA (qp_panel.hip): it is held to
-north_star's 1e-10 relative on x and f (identical status and iteration counts), and the same
-shapes are also checked bitwise with QPGPU_FLAG_EXACT."""
+Bar (north_star, per QP): status and l1-pass count identical, ||x - x_ref||_inf / ||x_ref||_inf
+<= 1e-10 and |f - f_ref| / |f_ref| <= 1e-10 — the PLAIN relative error, asserted for every build
+that produces a bench line's `value` — and, for every path that keeps the reference's operation
+order, x and f BITWISE identical.  The one tolerance path is the default n > 64 one, whose setup
+runs as blocked f64 MFMA (qp_panel.hip): held to the plain 1e-10 on x and f (identical status and
+iteration counts), and the same shapes are also checked bitwise with QPGPU_FLAG_EXACT.
+
+The QPGPU_FLAG_FAST builds (opt-in, not a bench line's value since round 5) have a weaker
+documented contract, asserted separately below (assert_fast_parity): x within the plain 1e-10,
+f within 1e-10 of its terms max(|f_ref|, 0.5|x'Gx| + |g0'x|)."""
 import json
 import os
 
@@ -23,20 +27,20 @@ TOL = 1e-10  # north_star: "within 1e-10 relative"
 
 def _relerr(xg, xo, fg, fo, ok, pr=None):
     """north_star's criterion per QP (qpgpu.rel_error_per_qp): the max over the QPs of
-    ||x - x_ref||_inf / ||x_ref||_inf (over the `ok` QPs, whose x is defined) and of
-    |f - f_ref| / max(|f_ref|, 0.5 |x^T G x| + |g0^T x|) (every QP) — the objective relative to the
-    magnitude of its terms, the scale the reference's own f is determined to when they cancel
-    (e.g. C1 seed 2026 holds a QP with f = 1.8e-5 from terms of +-0.628).  Given `pr` (its
-    original G), also returns the plain |f - f_ref| / |f_ref| maximum for the failure message."""
-    scale = None
+    ||x - x_ref||_inf / ||x_ref||_inf (over the `ok` QPs, whose x is defined) and of the plain
+    |f - f_ref| / |f_ref| (every QP).  Given `pr` (its original G), also the max of |f - f_ref|
+    relative to the objective's terms max(|f_ref|, 0.5 |x^T G x| + |g0^T x|) — the fast builds'
+    contract and an extra figure for the failure message."""
+    ex, _ = qpgpu.rel_error_per_qp(xg[ok], xo[ok], fg[ok], fo[ok])
+    _, efp = qpgpu.rel_error_per_qp(xg, xo, fg, fo)
+    mx = lambda a: float(a.max()) if a.size else 0.0
+    eft = None
     if pr is not None:
         scale = np.zeros(len(fo))
         scale[ok] = qpgpu.objective_term_scale(pr.G[ok], pr.g0[ok], xo[ok])
-    ex, _ = qpgpu.rel_error_per_qp(xg[ok], xo[ok], fg[ok], fo[ok])
-    _, ef = qpgpu.rel_error_per_qp(xg, xo, fg, fo, f_scale=scale)
-    _, efp = qpgpu.rel_error_per_qp(xg, xo, fg, fo)
-    mx = lambda a: float(a.max()) if a.size else 0.0
-    return mx(ex), mx(ef), mx(efp)
+        _, ef = qpgpu.rel_error_per_qp(xg, xo, fg, fo, f_scale=scale)
+        eft = mx(ef)
+    return mx(ex), mx(efp), eft
 
 
 def _bit_mismatch(a, b, show=6):
@@ -85,8 +89,8 @@ def assert_parity(pr, label, max_iter=0, write_factor=False, family=None, layout
     assert np.array_equal(so, sg), f"{label}: status differs at {np.where(so != sg)[0][:10]}"
     assert np.array_equal(io, ig), f"{label}: iteration count differs at {np.where(io != ig)[0][:10]}"
     ok = so != qpgpu.QP_NOT_POSITIVE_DEFINITE  # x untouched on that exit (reference throws)
-    ex, ef, efp = _relerr(xg, xo, fg, fo, ok, pr)
-    assert ex <= TOL and ef <= TOL, f"{label}: rel err x {ex:.3e} f {ef:.3e} (plain |df|/|f| {efp:.3e})"
+    ex, ef, eft = _relerr(xg, xo, fg, fo, ok, pr)
+    assert ex <= TOL and ef <= TOL, f"{label}: rel err x {ex:.3e} f {ef:.3e} (f vs its terms {eft:.3e})"
     if not bitwise_expected(pr.n, pr.m, write_factor, exact):
         return so, io
     bx, bf = _bit_mismatch(xg[ok], xo[ok]), _bit_mismatch(fg, fo)
@@ -306,8 +310,10 @@ def test_c5_bench_problems_parity(gpu, exact):
         assert (so == qpgpu.QP_OK).all() and io.min() > 50, (so, io)
 
 
-# ---- QPGPU_FLAG_FAST (the lane kernel's fast build): north_star's 1e-10 on x and f,
-# same status and l1-pass counts, on every shape the lane kernel covers
+# ---- QPGPU_FLAG_FAST (the lane kernel's fast build): same status and l1-pass counts;
+# x within north_star's plain 1e-10; f within 1e-10 of its terms (the fast builds' documented
+# contract — the plain |df|/|f| bar needs the reference's own rounding on QPs whose f cancels,
+# DESIGN §3.3, which is why no bench line's value comes from these builds)
 
 def assert_fast_parity(pr, label, layout=None, decisions=True, family=None):
     prc = qpgpu.Problems(pr.n, pr.p, pr.m, pr.G.copy(), pr.g0, pr.CE, pr.ce0, pr.CI, pr.ci0)
@@ -319,9 +325,9 @@ def assert_fast_parity(pr, label, layout=None, decisions=True, family=None):
         assert np.array_equal(io, ig), f"{label}: l1-pass count differs at {np.where(io != ig)[0][:10]}"
     ok = so == qpgpu.QP_OK
     sub = qpgpu.Problems(pr.n, pr.p, pr.m, pr.G[ok], pr.g0[ok], pr.CE[ok], pr.ce0[ok], pr.CI[ok], pr.ci0[ok])
-    ex, ef, efp = _relerr(xg[ok], xo[ok], fg[ok], fo[ok], np.ones(int(ok.sum()), dtype=bool), sub)
-    assert ex <= TOL and ef <= TOL, f"{label}: rel err x {ex:.3e} f {ef:.3e} (plain |df|/|f| {efp:.3e})"
-    return ex, ef
+    ex, efp, eft = _relerr(xg[ok], xo[ok], fg[ok], fo[ok], np.ones(int(ok.sum()), dtype=bool), sub)
+    assert ex <= TOL and eft <= TOL, f"{label}: rel err x {ex:.3e} f vs its terms {eft:.3e} (plain |df|/|f| {efp:.3e})"
+    return ex, eft
 
 
 @pytest.mark.parametrize("layout", ["qp_major", "tiled64"])
@@ -367,36 +373,16 @@ def test_fast_flag_rules(gpu):
     assert np.array_equal(xf.view(np.uint64), xd.view(np.uint64)) and np.array_equal(sf, sd)
 
 
-def test_fast_fallback_is_bounded(gpu):
+def test_fast_fallback_parity(gpu):
     """Every wave of a full C1 batch holds one QP whose G is non-finite, so every wave's fast
-    attempt turns invalid in the setup and the wave re-solves with the IEEE forms.  The fast
-    attempt stops at its first check (after the equality phase) instead of running its loop on
-    garbage, so the poisoned batch costs about a setup more than a clean one — held here to under
-    2.5x the clean batch's kernel time — and its results still meet the fast contract."""
-    import torch
-
+    attempt turns invalid in the setup and the wave re-solves with the IEEE forms: the results
+    still meet the fast contract.  (What the fallback costs in time is measured by
+    tools/fallback_cost.py, not asserted in the parity suite.)"""
     B = 65536
     pr = qpgpu.make_problems("general", 7, 6, 14, 0, B, seed=31)
     bad = qpgpu.Problems(pr.n, pr.p, pr.m, pr.G.copy(), pr.g0, pr.CE, pr.ce0, pr.CI, pr.ci0)
     bad.G[5::64, 0, 0] = np.nan
-
-    def kernel_ms(p_):
-        db = qpgpu.DeviceBatch(p_, "cuda:0", with_iters=False)
-        s = torch.cuda.current_stream()
-        go = db.launcher(s, fast=True)
-        go()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        for _ in range(10):
-            go()
-        e1.record(s)
-        torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / 10
-
-    t_clean, t_bad = kernel_ms(pr), kernel_ms(bad)
-    assert t_bad < 2.5 * t_clean, f"fallback batch {t_bad:.3f} ms vs clean {t_clean:.3f} ms"
-    assert_fast_parity(bad.slice(0, 4096), "fast fallback (NaN G in every wave)")
+    assert_fast_parity(bad, "fast fallback (NaN G in every wave)")
 
 
 # ---- QPGPU_FLAG_FAST for the wave kernel's LDS variants (n <= 64, m <= 256; DESIGN §5.7): the
@@ -485,3 +471,24 @@ def test_generic_beyond_specialised_shapes(gpu, kind, n, p, m, B, write_factor):
     assert qpgpu.kernel_name(n, p, m).startswith("qp_generic")
     assert_parity(qp_cases.make(kind, n, p, m, B, seed=n + m), f"generic {(n, p, m)}",
                   write_factor=write_factor)
+
+
+@pytest.mark.parametrize("layout,B", [("qp_major", 10), ("tiled64", 150)])
+def test_generic_sub_batches(gpu, layout, B):
+    """The generic kernel over sub-batches (its per-launch workspace capped, qpgpu_api.cpp): with
+    the cap lowered to three QPs' workspace, a batch runs as 3-QP launches (QP-major) or 64-QP
+    tile launches (TILED64), each with its inputs and outputs offset — bitwise as one launch."""
+    import ctypes
+
+    n, p, m = 40, 5, 90
+    qpgpu.LIB.qpk_generic_workspace_bytes.restype = ctypes.c_int64
+    qpgpu.LIB.qpk_generic_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64]
+    per = qpgpu.LIB.qpk_generic_workspace_bytes(n, m, 1)
+    setcap = qpgpu.LIB.qpgpu_debug_set_generic_ws_cap
+    setcap.argtypes = [ctypes.c_int64]
+    setcap(3 * per)
+    try:
+        assert_parity(qp_cases.make("general", n, p, m, B, seed=B), f"generic sub-batches B={B}",
+                      write_factor=True, family="generic", layout=layout)
+    finally:
+        setcap(0)

@@ -73,11 +73,14 @@ def test_kernel_name_flags_follow_the_flag_rules():
     assert nm(qpgpu.FLAG_FAST | qpgpu.FLAG_WRITE_FACTOR) == ""
     assert nm(qpgpu.FLAG_FORCE_LANE | qpgpu.FLAG_FORCE_WAVE) == ""
     assert nm(0x8) == ""
-    # the lane-pair family: fast build only, (7, 6, 14) only
-    assert nm(qpgpu.FLAG_FAST | qpgpu.FLAG_FORCE_PAIR) == "qp_pair_fast<N=7,P=6,M=14>"
-    assert nm(qpgpu.FLAG_FORCE_PAIR) == ""
-    assert nm(qpgpu.FLAG_FAST | qpgpu.FLAG_FORCE_PAIR | qpgpu.FLAG_FORCE_LANE) == ""
-    assert qpgpu.LIB.qpgpu_kernel_name_flags(7, 0, 14, qpgpu.FLAG_FAST | qpgpu.FLAG_FORCE_PAIR).decode() == ""
+    # the generic family has no fast build: FAST | FORCE_GENERIC launches (and names) the generic
+    # kernel, on every shape
+    for shape in ((7, 6, 14), (30, 6, 60), (14, 10, 28)):
+        g = qpgpu.LIB.qpgpu_kernel_name_flags(*shape, qpgpu.FLAG_FAST | qpgpu.FLAG_FORCE_GENERIC).decode()
+        assert g.startswith("qp_generic"), (shape, g)
+    # bit 0x1000 (the removed lane-pair family) is an unknown flag now
+    assert nm(qpgpu.FLAG_FAST | 0x1000) == ""
+    assert "qp_pair" not in open(qpgpu.LIB._name, "rb").read().decode("latin-1")
 
 
 def test_no_device_fails_loudly():

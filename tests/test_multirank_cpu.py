@@ -126,10 +126,45 @@ def test_bench_c4_split_and_cold_sets():
     assert bench.input_set_count(a, (bench.C4_GLOBAL // 2) * c1 // 65536) == 1
     assert bench.input_set_count(bench.parse(["--input-sets", "1"]), c1) == 1
     assert bench.metric_name("C1", 7, 6, 14, 65536, 1).startswith("QP solves/sec at n=7,p=6,m=14 batch=65536")
-    # the job's one gather by default; the fast lane build by default, --exact for the bitwise one
-    assert a.gather == "final" and a.fast and not a.exact
+    # the job's one gather by default; the bitwise builds by default (round 5), --fast opt-in
+    assert a.gather == "final" and not a.fast
     assert bench.parse(["--no-gather"]).gather == "none"
     assert bench.parse(["--gather", "every"]).gather == "every"
-    assert not bench.parse(["--exact"]).fast
+    assert bench.parse(["--fast"]).fast
     assert "n=30" in bench.metric_name("C3", 30, 6, 60, 65536, 1)
     assert "global batch=1048576 over 8" in bench.metric_name("C4", 7, 6, 14, 131072, 8)
+
+
+def test_bench_parity_record_is_the_plain_per_qp_bar():
+    """bench.parity_record gates on north_star's plain per-QP relative error (status identical,
+    ||dx||_inf/||x||_inf and |df|/|f| <= 1e-10 on every QP), in both layouts."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, PKG)
+    import bench
+    import qpgpu
+
+    pr = qpgpu.make_problems("general", 7, 6, 14, 0, 130, seed=4)
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((130, 7))
+    f = rng.standard_normal(130)
+    st = np.zeros(130, dtype=np.int32)
+    r = bench.parity_record(pr, "qp_major", (x, f, st), (x, f, st), "self")
+    assert r["meets_north_star"] and r["x_bitwise_equal"] and r["f_bitwise_equal"] and r["qps"] == 130
+    f2 = f.copy()
+    f2[77] *= 1 + 3e-10
+    r = bench.parity_record(pr, "qp_major", (x, f2, st), (x, f, st), "self")
+    assert not r["meets_north_star"] and r["qps_rel_err_f_above_tol"] == 1 and r["worst_f_qp"] == 77
+    x2 = x.copy()
+    x2[5, 3] += 1e-9 * np.abs(x[5]).max()
+    r = bench.parity_record(pr, "qp_major", (x2, f, st), (x, f, st), "self")
+    assert r["qps_rel_err_x_above_tol"] == 1 and r["qps_rel_err_f_above_tol"] == 0
+    # a device output in the TILED64 layout against a host reference, and against another
+    # device output in the same layout
+    xt = qpgpu.to_tiled64(x)
+    r = bench.parity_record(pr, "tiled64", (xt, f, st), (x, f, st), "self")
+    assert r["meets_north_star"] and r["x_bitwise_equal"]
+    r = bench.parity_record(pr, "tiled64", (xt, f, st), (xt, f, st), "self", ref_on_device=True)
+    assert r["meets_north_star"] and r["x_bitwise_equal"]
+    st2 = st.copy()
+    st2[3] = 1
+    assert bench.parity_record(pr, "qp_major", (x, f, st2), (x, f, st), "self")["status_equal"] == 129

@@ -22,7 +22,7 @@ MK
 SCHED=${SCHED_OVERRIDE-$SCHED}
 # the fast lane build is the same source with QPGPU_LANE_FAST (qp_lane_fast.hip) and contraction
 XF=""; case "$SRC" in qp_lane_fast|qp_wave_fast) XF="-ffp-contract=fast";; esac
-for f in qp_layout qp_lane qp_lane_fast qp_small qp_wave qp_wave_fast qp_panel qp_generic qp_pair qpgpu_api; do [ "$f" = "$SRC" ] || cp "$PKG/lib/$f.o" "$OUT/"; done
+for f in qp_layout qp_lane qp_lane_fast qp_small qp_wave qp_wave_fast qp_panel qp_generic qpgpu_api; do [ "$f" = "$SRC" ] || cp "$PKG/lib/$f.o" "$OUT/"; done
 (cd "$OUT/tmp" && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-fast-math -fPIC \
    -std=c++17 -I"$ROOT/include" -I"$PKG/csrc" $SCHED $XF "$@" -c "${SRCFILE:-$PKG/csrc/$SRC.hip}" -o "$OUT/$SRC.o" -save-temps 2>&1 | grep -v warning | grep -v "warnings\? generated" || true)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libqpgpu.so" "$OUT"/*.o

@@ -57,11 +57,15 @@ for s in $STEPS; do
     pmc)
       run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-c4 --streams 1
       run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o c1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-c4 --streams 1
-      python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" C1 65536 "$(python3 -c 'import sys; sys.path.insert(0,"motion-generation-using-quadratic-programs_amd"); import qpgpu; print(qpgpu.kernel_name(7,6,14,fast=True))')" "$OUT/pmc_traffic.json" ;;
+      python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" C1 65536 "$(python3 -c 'import sys; sys.path.insert(0,"motion-generation-using-quadratic-programs_amd"); import qpgpu; import os; print(qpgpu.kernel_name(7,6,14,fast=bool(os.environ.get("FAST"))))')" "$OUT/pmc_traffic.json" ;;
     stamps) for l in qp_major tiled64; do run stamps_general_$l 300 python tools/stamps.py general $l; run stamps_box_$l 300 python tools/stamps.py box $l; done ;;
     dist2) run dist2 600 python bench.py --gpus 2 --steps 10 --warmup 2 ;;
     dist2c1) run dist2c1 600 python bench.py --gpus 2 --config C1 --steps 10 --warmup 2 ;;
-    trace3) run trace3 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace3" -o c1 -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-c4 ;;
+    trace3)
+      # the default bench line's run (3 streams) under a kernel trace: do the timed steps' launches
+      # overlap (ms_per_step below the kernel's own duration)?  tools/trace_overlap.py
+      run trace3 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace3" -o c1 -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-c4
+      python3 tools/trace_overlap.py "$OUT/trace3/c1_kernel_trace.csv" qp_lane 5 20 "$OUT/trace3_overlap.json" > "$OUT/trace3_overlap.log" 2>&1; cat "$OUT/trace3_overlap.log" ;;
     profC3) run profC3 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profC3" -o c3 -- python3 bench.py --config C3 --steps 5 --warmup 1 --no-cpu --no-c4 --streams 1 --kernel-reps 3 ;;
     profC5) run profC5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profC5" -o c5 -- python3 bench.py --config C5 --steps 3 --warmup 1 --no-cpu --no-c4 --streams 1 --kernel-reps 2 ;;
     pmcC5)
@@ -138,7 +142,7 @@ PY
         case $c in C5) xa="--steps 2 --warmup 1 --kernel-reps 1";; C3) xa="--steps 3 --warmup 1 --kernel-reps 2";; *) xa="--steps 5 --warmup 1 --kernel-reps 3";; esac
         run pmc_fetch_$c 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$c" -o k -- python3 bench.py --config $c --no-cpu --no-c4 --streams 1 $xa
         run pmc_write_$c 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$c" -o k -- python3 bench.py --config $c --no-cpu --no-c4 --streams 1 $xa
-        read B K < <(python3 -c "import sys; sys.path.insert(0, 'motion-generation-using-quadratic-programs_amd'); import bench, qpgpu; c = bench.CONFIGS['$c']; print(c[4], qpgpu.kernel_name(c[1], c[2], c[3], fast=True))")
+        read B K < <(python3 -c "import sys; sys.path.insert(0, 'motion-generation-using-quadratic-programs_amd'); import bench, qpgpu; c = bench.CONFIGS['$c']; import os; print(c[4], qpgpu.kernel_name(c[1], c[2], c[3], fast=bool(os.environ.get('FAST'))))")
         python3 tools/pmc_traffic.py "$OUT/pmc_fetch_$c" "$OUT/pmc_write_$c" $c $B "$K" "$OUT/pmc_traffic.json"
       done ;;
     listctr) rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "listctr rc=$?" ;;

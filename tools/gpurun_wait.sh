@@ -6,7 +6,7 @@
 LOG=$1
 TO=$2
 shift 2
-for attempt in 1 2 3 4 5 6 7 8; do
+for attempt in $(seq 1 30); do
   timeout $((TO + 900)) /usr/local/graft/bin/gpurun --timeout "$TO" -- "$@" > "$LOG" 2>&1
   rc=$?
   if grep -q "stopped responding while being prepared\|slot(s) on this pod are busy\|backing off\|no box\|no free box\|taken away by the GPU service" "$LOG" &&
