@@ -98,6 +98,15 @@ constexpr int kScanDepth = 2;
 #ifndef QPGPU_LANE_DMA_P0
 #define QPGPU_LANE_DMA_P0 0
 #endif
+// The select that follows a scan computed inside the scan (1) or after it (0): the scan's last
+// loop, which finalises every s[i] while the rows past the LDS copy and ci0 are still in
+// registers, also tracks the first most-violated eligible constraint (the reference's strict-<
+// index-order scan from ss = 0 with no exclusions, which is what the select runs after a scan)
+// and keeps that column's entries of those rows — so the select issues no global loads.  The
+// same choice, the same values: bitwise unchanged.
+#ifndef QPGPU_LANE_PRESEL
+#define QPGPU_LANE_PRESEL 0
+#endif
 // A/B builds only (tools/ab_build.sh): the fast build's invalid-fast-form exit also at the top of
 // every loop pass (DESIGN §5.6 — why the product build has it after the equality phase only);
 // 2: the same check compiled in but never taken at run time (max_steps is never below -1)
@@ -846,6 +855,14 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
     int ip = 0, steps = 0;
     double ss = 0.0, ci0ip = 0.0;
     bool need_scan = true, need_select = true;
+    // QPGPU_LANE_PRESEL: the select's result prepared by the last scan (pre_ok), its constraint,
+    // its s and the entries of its column in the rows past the LDS copy (the last one: ci0)
+    constexpr int kNG = NM + 1 - kCiRows;
+    [[maybe_unused]] bool pre_ok = false;
+    [[maybe_unused]] int pre_ip = 0;
+    [[maybe_unused]] double pre_ss = 0.0, pre_v[kNG];
+#pragma unroll
+    for (int g = 0; g < kNG; g++) pre_v[g] = 0.0;
     bool active = !done;
     const int max_steps = a.max_steps;
     const double* CIg = view(const_cast<double*>(a.CI), n * m);
@@ -968,6 +985,29 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
                   sv[i] += gbuf[NG - 1][i];
                   psi += (sv[i] < 0.0) ? sv[i] : 0.0;
                 }
+              if constexpr (QPGPU_LANE_PRESEL != 0) {
+                // the select after this scan (ss = 0, no exclusions; `act` marks this scan's
+                // active set): first minimum below 0 among the inactive constraints
+                double bs = 0.0;
+                int bi = 0;
+                double bv[NG];
+#pragma unroll
+                for (int g = 0; g < NG; g++) bv[g] = 0.0;
+#pragma unroll
+                for (int i = 0; i < MM; i++)
+                  if (i < m) {
+                    const bool take = sv[i] < bs && !((act >> i) & 1ull);
+                    bs = take ? sv[i] : bs;
+                    bi = take ? i : bi;
+#pragma unroll
+                    for (int g = 0; g < NG; g++) bv[g] = take ? gbuf[g][i] : bv[g];
+                  }
+                pre_ss = bs;
+                pre_ip = bi;
+#pragma unroll
+                for (int g = 0; g < NG; g++) pre_v[g] = bv[g];
+                pre_ok = true;
+              }
             } else {
               // the first scan without the DMA (and every scan of the shapes without an
               // on-chip copy): software-pipelined two rows deep; row r lands in rowbuf[r % D]
@@ -1041,25 +1081,39 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
       nloop++;
       // ---- l2: pick the most violated constraint (ss deliberately not reset: reference quirk)
       if (active && need_select) {
+        if (QPGPU_LANE_PRESEL != 0 && pre_ok) {
+          // prepared by the scan just run (ss was 0 and excl empty there)
+          ss = pre_ss;
+          ip = pre_ip;
+        } else {
 #pragma unroll
-        for (int i = 0; i < MM; i++)
-          if (i < m) {
-            const bool elig = !((act >> i) & 1ull) && !((excl >> i) & 1ull);
-            const bool take = sv[i] < ss && elig;
-            ss = take ? sv[i] : ss;
-            ip = take ? i : ip;
-          }
+          for (int i = 0; i < MM; i++)
+            if (i < m) {
+              const bool elig = !((act >> i) & 1ull) && !((excl >> i) & 1ull);
+              const bool take = sv[i] < ss && elig;
+              ss = take ? sv[i] : ss;
+              ip = take ? i : ip;
+            }
+        }
         if (ss >= 0.0) {
           active = false;  // optimal
         } else {
+          if (QPGPU_LANE_PRESEL != 0 && pre_ok) {
 #pragma unroll
-          for (int j = 0; j < NM; j++)
-            npv[j] = (j < n) ? ((j < kCiRows && ci_ready) ? ci_lds_at(j * MM + ip) : ldCI(j * m + ip)) : 0.0;
-          ci0ip = ldci0(ip);
+            for (int j = 0; j < NM; j++)
+              npv[j] = (j < n) ? (j < kCiRows ? ci_lds_at(j * MM + ip) : pre_v[j - kCiRows < kNG ? j - kCiRows : 0]) : 0.0;
+            ci0ip = pre_v[kNG - 1];
+          } else {
+#pragma unroll
+            for (int j = 0; j < NM; j++)
+              npv[j] = (j < n) ? ((j < kCiRows && ci_ready) ? ci_lds_at(j * MM + ip) : ldCI(j * m + ip)) : 0.0;
+            ci0ip = ldci0(ip);
+          }
           lput_lo<IQLO>(uv, iq, 0.0);
           lput_lo<IQLO>(Av, iq, ip);
         }
       }
+      pre_ok = false;
       if (kStamps && a.stamps) {
         // make the select's loads part of the select span
         const double sink = npv[0] + ci0ip;
