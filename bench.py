@@ -658,6 +658,7 @@ def main():
         "l1_pass_histogram": hist,
         "status_ok_frac": st_ok,
         "outputs_consistent": consistent,
+        "build": qpgpu.build_provenance(),
     }
     if other:
         out["other_arithmetic"] = other

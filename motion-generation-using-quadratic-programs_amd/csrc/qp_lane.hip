@@ -98,20 +98,21 @@ constexpr int kScanDepth = 2;
 #ifndef QPGPU_LANE_DMA_P0
 #define QPGPU_LANE_DMA_P0 0
 #endif
-// The select that follows a scan computed inside the scan (1) or after it (0): the scan's last
-// loop, which finalises every s[i] while the rows past the LDS copy and ci0 are still in
-// registers, also tracks the first most-violated eligible constraint (the reference's strict-<
-// index-order scan from ss = 0 with no exclusions, which is what the select runs after a scan)
-// and keeps that column's entries of those rows — so the select issues no global loads.  The
-// same choice, the same values: bitwise unchanged.
-#ifndef QPGPU_LANE_PRESEL
-#define QPGPU_LANE_PRESEL 0
+// Where the DMA path touches the CI rows past the LDS copy and ci0 (one dword per 128-B line)
+// ahead of the first scan: 0 = nowhere, the first scan loads them (the product since round 5),
+// 1 = after the CE -> AGPR move (rounds 3-4), 2 = at the last equality step.  Measured on C1
+// (profiles/r05_s3): FETCH 146.4 / 125.0 / 130.1 MB for 1 / 0 / 2 — the touched lines leave L2
+// before the first scan reads them, so the touch only adds a second fetch — at 44.6 / 44.8 /
+// 45.7 us (two runs each; 0 and 1 within the run-to-run spread).
+#ifndef QPGPU_LANE_WARMUP
+#define QPGPU_LANE_WARMUP 0
 #endif
-// A/B builds only (tools/ab_build.sh): the fast build's invalid-fast-form exit also at the top of
-// every loop pass (DESIGN §5.6 — why the product build has it after the equality phase only);
-// 2: the same check compiled in but never taken at run time (max_steps is never below -1)
+// The fast build's invalid-fast-form check at the top of every loop pass as well (1, the
+// product since round 5) or only after the equality phase and after the loop (0); 2 = compiled
+// in but never taken (A/B only).  Round 4 dropped it after a wrong-result run that no committed
+// source reproduces (profiles/r05_s2, r05_s3).
 #ifndef QPGPU_LANE_LOOPTOP_EXIT
-#define QPGPU_LANE_LOOPTOP_EXIT 0
+#define QPGPU_LANE_LOOPTOP_EXIT 1
 #endif
 
 // ---- arithmetic of the fast build (frcp, rcp_ok, ldiv_r, ldiv, ldistance): qp_common.h,
@@ -219,7 +220,9 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
   // the rows past the LDS copy (which the scans keep reading from L2)
   constexpr int kPfCI = (NM * MM * 8 + 127) / 128 + 1, kPfC0 = (MM * 8 + 127) / 128 + 1;
   [[maybe_unused]] uint32_t pf[kPfCI + kPfC0];
+  bool warmed = false;  // the warm-up loads were issued (they retire after the equality phase)
   auto warmup = [&]() {
+    warmed = true;
     if (live) {
       const int off = dma ? kCiRows * MM * 8 : 0;  // (repeats the last line when shorter)
       const char* c = reinterpret_cast<const char*>(a.CI + b * (int64_t)(n * m)) + off;
@@ -370,7 +373,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
           // the rows past the LDS copy (and ci0) warmed here; the copy itself goes a part per
           // equality step.  Measured (profiles/r03_s10): C1 kernel 47.4 us with the warm-up
           // here, 48.6 without it, 49.9 with it at the first equality step
-          warmup();
+          if constexpr (QPGPU_LANE_WARMUP == 1) warmup();
         }
       }
     }
@@ -721,6 +724,9 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
   for (int i = 0; i <= NM; i++) {
     if constexpr (kCiDma && PX > 0) {
       if (ce_agpr && i < PX) dma_ci_part(i, PX);  // every lane (the copy is per wave)
+      if constexpr (QPGPU_LANE_WARMUP == 2) {
+        if (ce_agpr && i == PX - 1) warmup();
+      }
     }
     if (i < p && !done) {
       iq = i;
@@ -800,7 +806,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
     a.st_eq[b] = status;
   }
   if constexpr (T == 1 && (kLanePrefetch || kCiDma)) {
-    if (live && (dma || kLanePrefetch))  // the warm-up loads retire here, long after they landed
+    if (live && warmed)  // the warm-up loads retire here, long after they landed
 #pragma unroll
       for (int k = 0; k < kPfCI + kPfC0; k++) asm volatile("" ::"v"(pf[k]));
   }
@@ -822,11 +828,8 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
   // Fast build: a fast form that went out of range in the setup or the equality phase (or
   // non-finite data) sends the wave to the IEEE re-solve now, instead of after a loop that
   // would run on garbage up to the step cap.  (The CE / CI copies into LDS have landed: the
-  // re-solve may restage.)  The same check at the top of every loop pass was measured to change
-  // results: with it, qp_lane_fast<N=8,M=16> returned x off by up to 4e-2 relative on 4 of 1 001
-  // QPs with the same status and pass counts and no fallback taken (profiles/r04_s2), a
-  // code-generation effect we did not localise — so the loop keeps its single check after the
-  // last pass.
+  // re-solve may restage.)  The loop checks again at the top of every pass
+  // (QPGPU_LANE_LOOPTOP_EXIT) and after the last one.
   if constexpr (F) {
     if (wave_any(!fok)) return false;
   }
@@ -855,14 +858,6 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
     int ip = 0, steps = 0;
     double ss = 0.0, ci0ip = 0.0;
     bool need_scan = true, need_select = true;
-    // QPGPU_LANE_PRESEL: the select's result prepared by the last scan (pre_ok), its constraint,
-    // its s and the entries of its column in the rows past the LDS copy (the last one: ci0)
-    constexpr int kNG = NM + 1 - kCiRows;
-    [[maybe_unused]] bool pre_ok = false;
-    [[maybe_unused]] int pre_ip = 0;
-    [[maybe_unused]] double pre_ss = 0.0, pre_v[kNG];
-#pragma unroll
-    for (int g = 0; g < kNG; g++) pre_v[g] = 0.0;
     bool active = !done;
     const int max_steps = a.max_steps;
     const double* CIg = view(const_cast<double*>(a.CI), n * m);
@@ -985,29 +980,6 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
                   sv[i] += gbuf[NG - 1][i];
                   psi += (sv[i] < 0.0) ? sv[i] : 0.0;
                 }
-              if constexpr (QPGPU_LANE_PRESEL != 0) {
-                // the select after this scan (ss = 0, no exclusions; `act` marks this scan's
-                // active set): first minimum below 0 among the inactive constraints
-                double bs = 0.0;
-                int bi = 0;
-                double bv[NG];
-#pragma unroll
-                for (int g = 0; g < NG; g++) bv[g] = 0.0;
-#pragma unroll
-                for (int i = 0; i < MM; i++)
-                  if (i < m) {
-                    const bool take = sv[i] < bs && !((act >> i) & 1ull);
-                    bs = take ? sv[i] : bs;
-                    bi = take ? i : bi;
-#pragma unroll
-                    for (int g = 0; g < NG; g++) bv[g] = take ? gbuf[g][i] : bv[g];
-                  }
-                pre_ss = bs;
-                pre_ip = bi;
-#pragma unroll
-                for (int g = 0; g < NG; g++) pre_v[g] = bv[g];
-                pre_ok = true;
-              }
             } else {
               // the first scan without the DMA (and every scan of the shapes without an
               // on-chip copy): software-pipelined two rows deep; row r lands in rowbuf[r % D]
@@ -1081,39 +1053,25 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
       nloop++;
       // ---- l2: pick the most violated constraint (ss deliberately not reset: reference quirk)
       if (active && need_select) {
-        if (QPGPU_LANE_PRESEL != 0 && pre_ok) {
-          // prepared by the scan just run (ss was 0 and excl empty there)
-          ss = pre_ss;
-          ip = pre_ip;
-        } else {
 #pragma unroll
-          for (int i = 0; i < MM; i++)
-            if (i < m) {
-              const bool elig = !((act >> i) & 1ull) && !((excl >> i) & 1ull);
-              const bool take = sv[i] < ss && elig;
-              ss = take ? sv[i] : ss;
-              ip = take ? i : ip;
-            }
-        }
+        for (int i = 0; i < MM; i++)
+          if (i < m) {
+            const bool elig = !((act >> i) & 1ull) && !((excl >> i) & 1ull);
+            const bool take = sv[i] < ss && elig;
+            ss = take ? sv[i] : ss;
+            ip = take ? i : ip;
+          }
         if (ss >= 0.0) {
           active = false;  // optimal
         } else {
-          if (QPGPU_LANE_PRESEL != 0 && pre_ok) {
 #pragma unroll
-            for (int j = 0; j < NM; j++)
-              npv[j] = (j < n) ? (j < kCiRows ? ci_lds_at(j * MM + ip) : pre_v[j - kCiRows < kNG ? j - kCiRows : 0]) : 0.0;
-            ci0ip = pre_v[kNG - 1];
-          } else {
-#pragma unroll
-            for (int j = 0; j < NM; j++)
-              npv[j] = (j < n) ? ((j < kCiRows && ci_ready) ? ci_lds_at(j * MM + ip) : ldCI(j * m + ip)) : 0.0;
-            ci0ip = ldci0(ip);
-          }
+          for (int j = 0; j < NM; j++)
+            npv[j] = (j < n) ? ((j < kCiRows && ci_ready) ? ci_lds_at(j * MM + ip) : ldCI(j * m + ip)) : 0.0;
+          ci0ip = ldci0(ip);
           lput_lo<IQLO>(uv, iq, 0.0);
           lput_lo<IQLO>(Av, iq, ip);
         }
       }
-      pre_ok = false;
       if (kStamps && a.stamps) {
         // make the select's loads part of the select span
         const double sink = npv[0] + ci0ip;

@@ -117,6 +117,34 @@ def _load():
 LIB = _load()
 
 
+def build_provenance() -> dict:
+    """Which sources the loaded libqpgpu.so was built from: the md5 of the library, the sha256 the
+    Makefile recorded over its sources at link time (lib/libqpgpu.sources), the sha256 of those
+    files now, and whether they match (False: the library is older than its sources — rebuild;
+    None: the record or the sources are absent, e.g. an A/B library)."""
+    import hashlib
+
+    rec = os.path.join(os.path.dirname(LIB_PATH), "libqpgpu.sources")
+    out = {"lib": os.path.relpath(LIB_PATH, os.path.dirname(LIB_DIR)),
+           "lib_md5": hashlib.md5(open(LIB_PATH, "rb").read()).hexdigest(),
+           "sources_sha256_at_build": None, "sources_sha256_now": None, "matches_sources": None}
+    try:
+        files, sha = open(rec).read().split("\n")[:2]
+    except (OSError, ValueError):
+        return out
+    out["sources_sha256_at_build"] = sha.strip()
+    pkg = os.path.dirname(LIB_DIR)
+    try:
+        h = hashlib.sha256()
+        for f in files.split():
+            h.update(open(os.path.join(pkg, f), "rb").read())
+        out["sources_sha256_now"] = h.hexdigest()
+        out["matches_sources"] = out["sources_sha256_now"] == out["sources_sha256_at_build"]
+    except OSError:
+        pass
+    return out
+
+
 def kernel_name(n: int, p: int, m: int, fast: bool = False) -> str:
     if fast:
         return LIB.qpgpu_kernel_name_flags(n, p, m, FLAG_FAST).decode()

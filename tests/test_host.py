@@ -148,3 +148,14 @@ def test_tiled64_roundtrip_host():
         b, e = B - 1, 20
         assert t[(b // 64) * 64 * 21 + e * 64 + b % 64] == a.reshape(B, 21)[b, e]
         assert np.array_equal(qpgpu.from_tiled64(t, B, (7, 3)), a)
+
+
+def test_library_built_from_the_current_sources():
+    """The in-tree libqpgpu.so was linked from the sources in the tree (the Makefile records their
+    sha256, qpgpu.build_provenance): a stale library — the round-4 wrong-result run came from one
+     — fails here instead of being measured."""
+    if os.environ.get("QPGPU_LIB_PATH"):
+        pytest.skip("an A/B library is loaded")
+    prov = qpgpu.build_provenance()
+    assert prov["sources_sha256_at_build"], prov
+    assert prov["matches_sources"], f"libqpgpu.so is older than its sources: rebuild ({prov})"

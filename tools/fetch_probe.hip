@@ -13,6 +13,8 @@
 //   lane_x4        lane t reads its own 1792-B QP record with dwordx4 (per-lane blocks, stride 1792)
 //   lane_x2        the same records with 8-B loads (dwordx2)
 //   lane_lds       the same records by per-lane global_load_lds_dwordx4 (the CI-row copy)
+//   lane_touch4    lane t loads ONE dword per 128-B line of its record (the lane kernel's CI /
+//                  ci0 warm-up): the lines move, 4 B per line reach a register
 //   store_lane_x2  lane t writes its own 56-B x record with 8-B stores (x, stride 56)
 //   store_x2       lane t writes 8 B at base + 8 t (f)
 #include <hip/hip_runtime.h>
@@ -96,6 +98,16 @@ __global__ void __launch_bounds__(64) lane_lds(const char* __restrict__ src, int
   if (buf[threadIdx.x * 2] == 12345.678) out[0] = buf[threadIdx.x];
 }
 
+__global__ void __launch_bounds__(64) lane_touch4(const char* __restrict__ src, int64_t nrec, double* out) {
+  const int64_t r = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (r >= nrec) return;
+  const char* p = src + r * kRec;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < kRec / 128; k++) acc += *reinterpret_cast<const uint32_t*>(p + k * 128);
+  if (acc == 12345u) out[0] = acc;
+}
+
 __global__ void __launch_bounds__(64) store_lane_x2(double* __restrict__ dst, int64_t nrec) {
   const int64_t r = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (r >= nrec) return;
@@ -129,11 +141,12 @@ int main() {
     hipLaunchKernelGGL(lane_x4, dim3(blocks), dim3(64), 0, 0, b, nrec, out);
     hipLaunchKernelGGL(lane_x2, dim3(blocks), dim3(64), 0, 0, a, nrec, out);
     hipLaunchKernelGGL(lane_lds, dim3(blocks), dim3(64), 0, 0, b, nrec, out);
+    hipLaunchKernelGGL(lane_touch4, dim3(blocks), dim3(64), 0, 0, a, nrec, out);
     hipLaunchKernelGGL(store_lane_x2, dim3(blocks), dim3(64), 0, 0, (double*)a, nrec);
     hipLaunchKernelGGL(store_x2, dim3(blocks), dim3(64), 0, 0, (double*)b, nrec);
     CHECK(hipDeviceSynchronize());
   }
-  printf("read kernels: %lld bytes each (coalesced_x4, coalesced_lds, coalesced_x2, lane_x4, lane_x2, lane_lds)\n",
+  printf("read kernels: %lld bytes each (coalesced_x4, coalesced_lds, coalesced_x2, lane_x4, lane_x2, lane_lds, lane_touch4 (lines))\n",
          (long long)bytes);
   printf("store_lane_x2: %lld bytes; store_x2: %lld bytes\n", (long long)(nrec * 56), (long long)(nrec * 8));
   CHECK(hipFree(a));

@@ -13,7 +13,8 @@ import sys
 from collections import defaultdict
 
 NREC, REC = 1 << 18, 1792
-READ = {k: NREC * REC for k in ("coalesced_x4", "coalesced_lds", "coalesced_x2", "lane_x4", "lane_x2", "lane_lds")}
+READ = {k: NREC * REC for k in ("coalesced_x4", "coalesced_lds", "coalesced_x2", "lane_x4", "lane_x2", "lane_lds",
+                                  "lane_touch4")}  # lane_touch4: the lines it touches
 WRITE = {"store_lane_x2": NREC * 56, "store_x2": NREC * 8}
 
 
