@@ -107,13 +107,6 @@ constexpr int kScanDepth = 2;
 #ifndef QPGPU_LANE_WARMUP
 #define QPGPU_LANE_WARMUP 0
 #endif
-// Cooperative finish: once at most kCoopMax lanes of a wave still have a QP in
-// the active-set loop, each of those QPs moves to a 32-lane subgroup that finishes it with its
-// constraints and J rows spread over the lanes (qp_small's loop form, the same operations in the
-// same order: bitwise unchanged).  A wave's last passes then cost a fraction of a one-lane pass.
-#ifndef QPGPU_LANE_COOP
-#define QPGPU_LANE_COOP 1
-#endif
 // The fast build's invalid-fast-form check at the top of every loop pass as well (1, the
 // product since round 5) or only after the equality phase and after the loop (0); 2 = compiled
 // in but never taken (A/B only).  Round 4 dropped it after a wrong-result run that no committed
@@ -124,387 +117,6 @@ constexpr int kScanDepth = 2;
 
 // ---- arithmetic of the fast build (frcp, rcp_ok, ldiv_r, ldiv, ldistance): qp_common.h,
 // shared with the lane-pair kernel (qp_pair.hip).
-
-// The cooperative finish's loop for one QP (qp_lane's loop form → qp_small's: DESIGN §5.11), run
-// by a 32-lane subgroup (ls = 0..31) on the QP's state dumped in the region Q of the stage
-// buffer; its results go back to Q.  EXACT QP-major shapes (n = NM, m = MM); rows
-// 0..kCiRows-1 of the QP's CI are read from the lane-interleaved LDS copy of lane sl.
-template <int NM, int MM>
-struct CoopLay {
-  static constexpr int S = 32, MAXQ = 64 / S, RS = NM + 1;
-  static constexpr int O_R = 0, O_P = O_R + NM * RS, O_S = O_P + NM * RS, O_D = O_S + MM,
-                       O_Z = O_D + NM, O_NP = O_Z + NM, O_XO = O_NP + NM, O_UO = O_XO + NM,
-                       O_AO = O_UO + NM + 1, O_X = O_AO + NM + 1, O_U = O_X + NM, O_A = O_U + NM + 1,
-                       O_NPV = O_A + NM + 1, O_SC = O_NPV + NM, REG = O_SC + 16;
-};
-
-template <int NM, int MM, int kCiRows>
-__device__ __forceinline__ void coop_solve(const QpArgs& a, double* sbuf, double* Q, int ls, int p,
-                                                     int64_t b0) {
-  using L = CoopLay<NM, MM>;
-  constexpr int S = L::S, RS = L::RS, O_R = L::O_R, O_P = L::O_P, O_S = L::O_S, O_D = L::O_D,
-                O_Z = L::O_Z, O_NP = L::O_NP, O_XO = L::O_XO, O_UO = L::O_UO, O_AO = L::O_AO,
-                O_X = L::O_X, O_U = L::O_U, O_A = L::O_A, O_NPV = L::O_NPV, O_SC = L::O_SC;
-  constexpr int n = NM, m = MM;
-  const int max_steps = a.max_steps;
-  auto ubits = [](double v) { return __builtin_bit_cast(uint64_t, v); };
-    double* const Rm = Q + O_R;
-    double* const Pm = Q + O_P;
-    double* const sb = Q + O_S;
-    double* const db = Q + O_D;
-    double* const zb = Q + O_Z;
-    double* const npb = Q + O_NP;
-    // replicated state
-    int ciq = (int)Q[O_SC + 0];
-    uint64_t cact = ubits(Q[O_SC + 1]), cexcl = ubits(Q[O_SC + 2]);
-    int cip = (int)Q[O_SC + 3];
-    double css = Q[O_SC + 4];
-    const int fl = (int)Q[O_SC + 5];
-    bool cscan = (fl & 1) != 0, csel = (fl & 2) != 0;
-    int csteps = (int)Q[O_SC + 6], citer = (int)Q[O_SC + 7];
-    double cf = Q[O_SC + 8], cRn = Q[O_SC + 9];
-    const double cc1 = Q[O_SC + 10], cc2 = Q[O_SC + 11];
-    const int sl = (int)Q[O_SC + 12];
-    int cst = (int)Q[O_SC + 13];
-    // x, u, A, d, r in registers; z, np and the rollback copies (x_old, u_old, A_old) stay
-    // in the region (zb, npb, O_XO / O_UO / O_AO) and are read where they are used
-    double cx[NM], cu[NM + 1], cd[NM], cr[NM];
-    int cA[NM + 1];
-    double* const xob = Q + O_XO;
-    double* const uob = Q + O_UO;
-    double* const aob = Q + O_AO;
-#pragma unroll
-    for (int i = 0; i < NM; i++) {
-      cx[i] = Q[O_X + i];
-      cd[i] = cr[i] = 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i <= NM; i++) {
-      cu[i] = Q[O_U + i];
-      cA[i] = (int)Q[O_A + i];
-    }
-    // this lane's J row (k = ls) and constraint (c = ls): rows 0..kCiRows-1 of CI from the
-    // QP's LDS copy, the others and ci0 from its global block (loaded once)
-    double Jr[NM], CIr[NM];
-    const double* CIq = a.CI + (b0 + sl) * (int64_t)(n * m);
-    const double* ci0q = a.ci0 + (b0 + sl) * (int64_t)m;
-    const bool own_c = ls < m;
-    const int cc_ = own_c ? ls : 0;
-#pragma unroll
-    for (int j = 0; j < NM; j++) {
-      Jr[j] = ls < n ? Pm[ls * RS + j] : 0.0;
-      const int e = j * MM + cc_;
-      CIr[j] = j >= n ? 0.0
-                      : (j < kCiRows ? sbuf[((e >> 1) * kQpw + sl) * 2 + (e & 1)] : CIq[j * m + cc_]);
-    }
-    const double ci0r = ci0q[cc_];
-    double npo = ls < n ? Q[O_NPV + (ls < NM ? ls : 0)] : 0.0;
-    if (ls < NM) npb[ls] = Q[O_NPV + ls];
-    sg_sync();  // the J dump is read before P serves as compute_d's transpose
-    const double cinf = dinf();
-    auto csel_d = [&](const double(&v)[NM + 1], int i) { return lsel<NM + 1>(v, i); };
-    // compute_d: d[c] = sum_j J[j][c] np[j] (j ascending) through the transpose P
-    auto c_compute_d = [&]() {
-      if (ls < n) {
-#pragma unroll
-        for (int c = 0; c < NM; c++)
-          if (c < n) Pm[ls * RS + c] = Jr[c] * npo;
-      }
-      sg_sync();
-      if (ls < n) {
-        double s = 0.0;
-#pragma unroll
-        for (int j = 0; j < NM; j++)
-          if (j < n) s += Pm[j * RS + ls];
-        db[ls] = s;
-      }
-      sg_sync();
-#pragma unroll
-      for (int i = 0; i < NM; i++) cd[i] = (i < n) ? db[i] : 0.0;
-      sg_sync();
-    };
-    auto c_update_z = [&]() {
-      double z = 0.0;
-#pragma unroll
-      for (int j = 0; j < NM; j++)
-        if (j >= ciq && j < n) z += Jr[j] * cd[j];
-      if (ls < n) zb[ls] = z;
-      sg_sync();
-    };
-    auto c_update_r = [&]() {
-#pragma unroll
-      for (int i = NM - 1; i >= 0; i--) {
-        if (i >= p && i < ciq) {
-          double s = 0.0;
-#pragma unroll
-          for (int j = i + 1; j < NM; j++)
-            if (j < ciq) s += Rm[i * RS + j] * cr[j];
-          cr[i] = (cd[i] - s) / Rm[i * RS + i];
-        }
-      }
-    };
-    auto c_add = [&]() -> bool {
-      if (ciq >= n) return false;
-#pragma unroll
-      for (int j = NM - 1; j >= 1; j--) {
-        if (j <= n - 1 && j >= ciq + 1) {
-          double cc = cd[j - 1], sn = cd[j];
-          const double h = qp_distance(cc, sn);
-          if (!(fabs(h) < kEps)) {
-            cd[j] = 0.0;
-            sn = sn / h;
-            cc = cc / h;
-            if (cc < 0.0) {
-              cc = -cc;
-              sn = -sn;
-              cd[j - 1] = -h;
-            } else {
-              cd[j - 1] = h;
-            }
-            const double xny = sn / (1.0 + cc);
-            const double t1 = Jr[j - 1], t2 = Jr[j];
-            Jr[j - 1] = t1 * cc + t2 * sn;
-            Jr[j] = xny * (t1 + Jr[j - 1]) - t2;
-          }
-        }
-      }
-      ciq++;
-      if (ls == 0) {
-#pragma unroll
-        for (int i = 0; i < NM; i++)
-          if (i < ciq) Rm[i * RS + ciq - 1] = cd[i];
-      }
-      sg_sync();
-      const double dd = fabs(lsel<NM>(cd, ciq - 1));
-      if (dd <= kEps * cRn) return false;
-      cRn = (cRn < dd) ? dd : cRn;
-      return true;
-    };
-    auto c_delete = [&](int l) {
-      int qq = 0;
-      bool found = false;
-#pragma unroll
-      for (int k = 0; k <= NM; k++)
-        if (!found && k >= p && k < ciq && cA[k] == l) {
-          qq = k;
-          found = true;
-        }
-#pragma unroll
-      for (int i = 0; i < NM; i++)
-        if (i >= qq && i < ciq - 1) {
-          cA[i] = cA[i + 1];
-          cu[i] = cu[i + 1];
-        }
-      for (int j = ls; j < n; j += S)
-        for (int i = qq; i < ciq - 1; i++) Rm[j * RS + i] = Rm[j * RS + i + 1];
-      {
-        const int aiq = lsel<NM + 1>(cA, ciq);
-        const double uiq = csel_d(cu, ciq);
-        lput_lo<0>(cA, ciq - 1, aiq);
-        lput_lo<0>(cu, ciq - 1, uiq);
-        lput_lo<0>(cA, ciq, 0);
-        lput_lo<0>(cu, ciq, 0.0);
-      }
-      for (int j = ls; j < ciq; j += S) Rm[j * RS + ciq - 1] = 0.0;
-      ciq--;
-      sg_sync();
-      if (ciq == 0) return;
-#pragma unroll
-      for (int j = 0; j < NM - 1; j++) {
-        if (j >= qq && j < ciq) {
-          double cc = Rm[j * RS + j], sn = Rm[(j + 1) * RS + j];
-          const double h = qp_distance(cc, sn);
-          if (!(fabs(h) < kEps)) {
-            cc = cc / h;
-            sn = sn / h;
-            double nd;
-            if (cc < 0.0) {
-              nd = -h;
-              cc = -cc;
-              sn = -sn;
-            } else {
-              nd = h;
-            }
-            const double xny = sn / (1.0 + cc);
-            for (int k = j + 1 + ls; k < ciq; k += S) {
-              const double t1 = Rm[j * RS + k], t2 = Rm[(j + 1) * RS + k];
-              const double r1 = t1 * cc + t2 * sn;
-              Rm[j * RS + k] = r1;
-              Rm[(j + 1) * RS + k] = xny * (t1 + r1) - t2;
-            }
-            if (ls == 0) {
-              Rm[(j + 1) * RS + j] = 0.0;
-              Rm[j * RS + j] = nd;
-            }
-            const double t1 = Jr[j], t2 = Jr[j + 1];
-            Jr[j] = t1 * cc + t2 * sn;
-            Jr[j + 1] = xny * (Jr[j] + t1) - t2;
-          }
-          sg_sync();
-        }
-      }
-    };
-    while (true) {
-      if (cscan) {  // ---- l1
-        citer++;
-#pragma unroll
-        for (int k = 0; k < NM; k++)
-          if (k >= p && k < ciq) cact |= 1ull << cA[k];
-        if (own_c) {
-          double s = 0.0;
-#pragma unroll
-          for (int j = 0; j < NM; j++)
-            if (j < n) s += CIr[j] * cx[j];
-          s += ci0r;
-          sb[ls] = s;
-        }
-        sg_sync();
-        cexcl = 0;
-        css = 0.0;
-        cip = 0;
-        double psi = 0.0;
-#pragma unroll
-        for (int i = 0; i < MM; i++)
-          if (i < m) {
-            const double si = sb[i];
-            psi += (si < 0.0) ? si : 0.0;
-          }
-        if (fabs(psi) <= (double)m * kEps * cc1 * cc2 * 100.0) break;  // optimal
-        if (ls == 0) {
-#pragma unroll
-          for (int i = 0; i < NM; i++) {
-            if (i < ciq) {
-              uob[i] = cu[i];
-              aob[i] = (double)cA[i];
-            }
-            xob[i] = cx[i];
-          }
-        }
-        sg_sync();
-      }
-      if (csel) {  // ---- l2 (ss deliberately not reset: reference quirk)
-#pragma unroll
-        for (int i = 0; i < MM; i++)
-          if (i < m) {
-            const double si = sb[i];
-            const bool elig = !((cact >> i) & 1ull) && !((cexcl >> i) & 1ull);
-            if (si < css && elig) {
-              css = si;
-              cip = i;
-            }
-          }
-        if (css >= 0.0) break;  // optimal
-        if (ls == cip) {
-#pragma unroll
-          for (int j = 0; j < NM; j++)
-            if (j < n) npb[j] = CIr[j];
-        }
-        sg_sync();
-        npo = ls < n ? npb[ls < NM ? ls : 0] : 0.0;
-        lput_lo<0>(cu, ciq, 0.0);
-        lput_lo<0>(cA, ciq, cip);
-      }
-      // ---- l2a
-      if (max_steps > 0 && ++csteps > max_steps) {
-        cst = QPGPU_QP_MAX_ITER;
-        break;
-      }
-      c_compute_d();
-      c_update_z();
-      c_update_r();
-      int l = 0;
-      double t1 = cinf;
-#pragma unroll
-      for (int k = 0; k < NM; k++)
-        if (k >= p && k < ciq && cr[k] > 0.0) {
-          const double q_ = cu[k] / cr[k];
-          const bool take = q_ < t1;
-          t1 = take ? q_ : t1;
-          l = take ? opq_l(cA[k]) : l;
-        }
-      double zz = 0.0, znp = 0.0;
-#pragma unroll
-      for (int i = 0; i < NM; i++)
-        if (i < n) {
-          const double zi = zb[i], pi = npb[i];
-          zz += zi * zi;
-          znp += zi * pi;
-        }
-      double t2;
-      if (fabs(zz) > kEps) {
-        t2 = -sb[cip] / znp;
-        if (t2 < 0) t2 = cinf;  // Takano Akio patch
-      } else {
-        t2 = cinf;
-      }
-      const double t = (t2 < t1) ? t2 : t1;
-      if (t >= cinf) {
-        cst = QPGPU_QP_INFEASIBLE;
-        cf = cinf;
-        break;
-      }
-      if (t2 >= cinf) {  // dual step only
-#pragma unroll
-        for (int k = 0; k < NM; k++)
-          if (k >= p && k < ciq) cu[k] -= t * cr[k];
-        lput_lo<0>(cu, ciq, csel_d(cu, ciq) + t);
-        cact &= ~(1ull << l);
-        c_delete(l);
-        cscan = csel = false;
-        continue;
-      }
-      // primal and dual step
-#pragma unroll
-      for (int k = 0; k < NM; k++) cx[k] += t * (k < n ? zb[k] : 0.0);
-      cf += t * znp * (0.5 * t + csel_d(cu, ciq));
-#pragma unroll
-      for (int k = 0; k < NM; k++)
-        if (k >= p && k < ciq) cu[k] -= t * cr[k];
-      lput_lo<0>(cu, ciq, csel_d(cu, ciq) + t);
-      if (fabs(t - t2) < kEps) {  // full step
-        if (!c_add()) {
-          cexcl |= 1ull << cip;
-          c_delete(cip);
-          cact = 0;
-#pragma unroll
-          for (int i = 0; i < NM; i++)
-            if (i >= p && i < ciq) {
-              cA[i] = (int)aob[i];
-              cu[i] = uob[i];
-              cact |= 1ull << cA[i];
-            }
-#pragma unroll
-          for (int i = 0; i < NM; i++) cx[i] = xob[i];
-          cscan = false;
-          csel = true;
-        } else {
-          cact |= 1ull << cip;
-          cscan = csel = true;
-        }
-        continue;
-      }
-      // partial step: drop l, refresh s[ip]
-      cact &= ~(1ull << l);
-      c_delete(l);
-      if (ls == cip) {
-        double s = 0.0;
-#pragma unroll
-        for (int j = 0; j < NM; j++)
-          if (j < n) s += CIr[j] * cx[j];
-        sb[cip] = s + ci0r;
-      }
-      sg_sync();
-      cscan = csel = false;
-    }
-    // results for the QP's own lane
-    if (ls == 0) {
-#pragma unroll
-      for (int i = 0; i < NM; i++) Q[O_X + i] = cx[i];
-      Q[O_SC + 7] = (double)citer;
-      Q[O_SC + 8] = cf;
-      Q[O_SC + 13] = (double)cst;
-    }
-}
 
 // PX >= 0: p is the compile-time constant PX as well (C1/C4: 6, C2: 0), which folds every
 // [p, iq) loop of the active-set phase (for n = 7, p = 6 that range holds at most one entry).
@@ -1424,25 +1036,12 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
     };
     uint64_t tscan = 0, tsel = 0, nloop = 0, tfirst = 0;  // diagnostic stamps only
     [[maybe_unused]] uint64_t tdzr = 0, tstep = 0;        // (QPGPU_LANE_STAMPS == 2: l2a split)
-    // the cooperative finish needs the on-chip CI copy of the QP-major EXACT shapes and room for
-    // its two subgroup regions past that copy in the stage buffer
-    constexpr int kCoopS = 32, kCoopMax = 64 / kCoopS, kCoopRS = NM + 1;
-    constexpr int kCoopReg = 2 * NM * kCoopRS + MM + 3 * NM + 3 * NM + 2 + 4 * NM + 2 + 16;
-    constexpr bool kCoop = QPGPU_LANE_COOP && EXACT && T == 1 && kCiRows > 0 && MM <= kCoopS &&
-                           kCiRows * MM * kQpw + kCoopMax * kCoopReg <= STAGE;
-    bool coop_go = false;
     while (wave_any(active)) {
       if constexpr (F && QPGPU_LANE_LOOPTOP_EXIT == 1) {
         if (wave_any(!fok)) return false;
       }
       if constexpr (F && QPGPU_LANE_LOOPTOP_EXIT == 2) {
         if (wave_any(!fok) && a.max_steps < -1) return false;
-      }
-      if constexpr (kCoop) {
-        if (ci_ready && __builtin_popcountll(__builtin_amdgcn_ballot_w64(active)) <= kCoopMax) {
-          coop_go = true;
-          break;
-        }
       }
       const uint64_t tl0 = (kStamps && a.stamps) ? __builtin_amdgcn_s_memtime() : 0;
       scan_pass();
@@ -1580,83 +1179,6 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
             lput_lo<0>(sv, ip, s + ci0ip);
           }
           if (dual || part) need_scan = need_select = false;
-        }
-      }
-    }
-    // ---------------------------------------------------------------- cooperative finish
-    // The wave's remaining QPs (at most kCoopMax, each on its own lane) are dumped to LDS and
-    // finished by 32-lane subgroups in qp_small's form: lane c of the subgroup holds constraint c
-    // (the scan), lane k holds row k of J (compute_d through an LDS transpose, update_z, the
-    // rotations), everything else is replicated and computed identically by every lane (so the
-    // subgroup never diverges internally); R lives in LDS.  Every value is formed by the same
-    // operations in the same order as in the lane form above, so results are bit for bit the
-    // same.  The results go back through LDS to the QP's own lane, which writes the outputs.
-    if constexpr (kCoop) {
-      if (coop_go) {
-        using L = CoopLay<NM, MM>;
-        constexpr int RS = L::RS, O_R = L::O_R, O_P = L::O_P, O_S = L::O_S, O_XO = L::O_XO,
-                      O_UO = L::O_UO, O_AO = L::O_AO, O_X = L::O_X, O_U = L::O_U, O_A = L::O_A,
-                      O_NPV = L::O_NPV, O_SC = L::O_SC;
-        static_assert(L::REG == kCoopReg && L::MAXQ == kCoopMax, "coop region");
-        double* const cbase = sbuf + kCiRows * MM * kQpw;
-        const uint64_t am = __builtin_amdgcn_ballot_w64(active);
-        const int na = __builtin_popcountll(am);
-        auto bits = [](uint64_t v) { return __builtin_bit_cast(double, v); };
-        // ---- dump (the QP's own lane)
-        if (active) {
-          const int rk = __builtin_popcountll(am & ((1ull << lane) - 1));
-          double* const Q = cbase + rk * kCoopReg;
-#pragma unroll
-          for (int i = 0; i < NM; i++) {
-#pragma unroll
-            for (int j = 0; j < NM; j++) {
-              Q[O_R + i * RS + j] = RI::at(i, j) >= 0 ? Rv[RI::at(i, j) >= 0 ? RI::at(i, j) : 0] : 0.0;
-              Q[O_P + i * RS + j] = Jreg[i][j];
-            }
-            Q[O_XO + i] = xold[i];
-            Q[O_X + i] = xv[i];
-            Q[O_NPV + i] = npv[i];
-          }
-#pragma unroll
-          for (int i = 0; i < NM; i++) {
-            Q[O_UO + i] = uold[i];
-            Q[O_AO + i] = (double)aold[i];
-          }
-#pragma unroll
-          for (int i = 0; i <= NM; i++) {
-            Q[O_U + i] = uv[i];
-            Q[O_A + i] = (double)Av[i];
-          }
-#pragma unroll
-          for (int i = 0; i < MM; i++) Q[O_S + i] = sv[i];
-          Q[O_SC + 0] = (double)iq;
-          Q[O_SC + 1] = bits(act);
-          Q[O_SC + 2] = bits(excl);
-          Q[O_SC + 3] = (double)ip;
-          Q[O_SC + 4] = ss;
-          Q[O_SC + 5] = (double)((need_scan ? 1 : 0) | (need_select ? 2 : 0));
-          Q[O_SC + 6] = (double)steps;
-          Q[O_SC + 7] = (double)iter;
-          Q[O_SC + 8] = fval;
-          Q[O_SC + 9] = R_norm;
-          Q[O_SC + 10] = c1;
-          Q[O_SC + 11] = c2;
-          Q[O_SC + 12] = (double)lane;
-          Q[O_SC + 13] = (double)status;
-        }
-        sg_sync();
-        const int g = lane / L::S;
-        if (g < na) coop_solve<NM, MM, kCiRows>(a, sbuf, cbase + g * kCoopReg, lane - g * L::S, p, b0);
-        sg_sync();
-        if (active) {
-          const int rk = __builtin_popcountll(am & ((1ull << lane) - 1));
-          const double* const Q = cbase + rk * kCoopReg;
-#pragma unroll
-          for (int i = 0; i < NM; i++) xv[i] = Q[O_X + i];
-          iter = (int)Q[O_SC + 7];
-          fval = Q[O_SC + 8];
-          status = (int)Q[O_SC + 13];
-          active = false;
         }
       }
     }
