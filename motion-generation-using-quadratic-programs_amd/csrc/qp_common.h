@@ -349,7 +349,9 @@ constexpr uint32_t kSetupDone = 0x40000000u;
 // Per-QP device workspace of the large-QP path (n > 64, qp_wave.hip GJR + qp_panel.hip):
 //   [0, OFF_R)        J, COLUMN-major: J[k][j] at j*JS + k
 //   [OFF_R, OFF_H)    R row-major (R[i][j] at i*JS + j); the setup's scratch for G -> L
-//   [OFF_H, PER_QP)   header: status, f0, c1, c2, (pad), x0 at HX
+//   [OFF_H, OFF_G)    header: status, f0, c1, c2, (pad), x0 at HX
+//   [OFF_G, PER_QP)   the Givens coefficients of a deferred add_constraint sweep while a second
+//                     one is pending (qp_wave.hip, tolerance mode: 4 per rotation)
 constexpr int kBigN = 256;
 template <int NMAX>
 struct BigWs {
@@ -357,7 +359,8 @@ struct BigWs {
   static constexpr int64_t OFF_R = (int64_t)NMAX * JS;
   static constexpr int64_t OFF_H = 2 * (int64_t)NMAX * JS;
   static constexpr int HX = 8;
-  static constexpr int64_t PER_QP = OFF_H + HX + NMAX;
+  static constexpr int64_t OFF_G = OFF_H + HX + NMAX;
+  static constexpr int64_t PER_QP = OFF_G + 4 * (int64_t)NMAX;
 };
 
 __device__ __forceinline__ void qp_stamp(const QpArgs& a, int slot) {

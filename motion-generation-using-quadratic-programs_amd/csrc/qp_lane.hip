@@ -104,6 +104,11 @@ constexpr int kScanDepth = 2;
 // (profiles/r05_s3): FETCH 146.4 / 125.0 / 130.1 MB for 1 / 0 / 2 — the touched lines leave L2
 // before the first scan reads them, so the touch only adds a second fetch — at 44.6 / 44.8 /
 // 45.7 us (two runs each; 0 and 1 within the run-to-run spread).
+// Where the setup waits for round B (CE / ce0 into LDS): 1 = after J = L^-T and the solve, which
+// need only the factor, 0 = right after the Cholesky (rounds 1-4; A/B only)
+#ifndef QPGPU_LANE_CE_LATE
+#define QPGPU_LANE_CE_LATE 1
+#endif
 #ifndef QPGPU_LANE_WARMUP
 #define QPGPU_LANE_WARMUP 0
 #endif
@@ -348,6 +353,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
           if (i < n && j < n) Gw[(i * n + j) * T] = Gr[i][j];
     }
     // round B lands: the staged CE / ce0 are read in the equality phase
+    auto land_round_b = [&]() {
     if (p > 0) {
       const int np_ = n * p;
       const int offc = (kQpw * np_ + 127) / 128 * 128;
@@ -377,6 +383,10 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
         }
       }
     }
+    };
+    // QPGPU_LANE_CE_LATE: wait for round B after J = L^-T and the solve (which need only the
+    // factor), so the CE transfer lands under them instead of stalling the wave after the Cholesky
+    if constexpr (!QPGPU_LANE_CE_LATE) land_round_b();
     if (chol_ok) {
       // J = L^{-T}: row r of J = L^{-1} e_r (forward_elimination); c2 = trace(J).
       // With a finite L the first r entries of L^{-1} e_r are exactly +0.0 (0.0 - L*(+0) and
@@ -449,6 +459,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
         if (i < n) fval += g0v[i] * xv[i];
       fval = 0.5 * fval;
     }
+    if constexpr (QPGPU_LANE_CE_LATE) land_round_b();
   }
   if constexpr (kCiDma && PX == 0) {
     // no equality phase to hide the copy behind: issued after the setup, all at once (the first

@@ -176,8 +176,9 @@ __device__ __forceinline__ void sg_argmin(double& v, int& i) {
 // coefficients loaded per chunk of rotations in the J sweep, two constraints per lane in the
 // l1 scan, the t1 selection across the four waves — DESIGN §5.3.)
 #ifndef QPGPU_WAVE_TOLLOOP
-#define QPGPU_WAVE_TOLLOOP 7  // bit 0: fused compute_d + update_z, bit 1: tree update_r,
-                              // bit 2: add_constraint J sweep deferred into the next d/z pass
+#define QPGPU_WAVE_TOLLOOP 15  // bit 0: fused compute_d + update_z, bit 1: tree update_r,
+                               // bit 2: add_constraint J sweep deferred into the next d/z pass,
+                               // bit 3: two sweeps deferred, J written back every second add
 #endif
 // v from the lane the DPP control CTRL selects (a full-row permutation: every lane valid)
 template <int CTRL>
@@ -749,6 +750,16 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
   // must first apply the pending sweep (plain_sweep with iq0 = pend).
   int pend = -1;
   constexpr bool kDefer = GJR && (QPGPU_WAVE_TOLLOOP & 4) && (QPGPU_WAVE_TOLLOOP & 1) && S == 4 * 64 && NMAX <= S;
+  // Two deferred sweeps (QPGPU_WAVE_TOLLOOP bit 3): the d/z pass after an add applies the
+  // pending sweep A in registers without writing J back; the next add's sweep B joins it and the
+  // pass after that applies A then B (B one rotation behind A along each row) and writes the
+  // final columns once — each trailing column of J is written once per two adds instead of once
+  // per add.  While B is pending, A's coefficients sit in the workspace (gA) because B's occupy
+  // gc.  pend2 = B's iq0 or -1; J in memory is current only with nothing pending, so
+  // delete_constraint and a degenerate add first apply what is pending.
+  constexpr bool kDefer2 = kDefer && (QPGPU_WAVE_TOLLOOP & 8);
+  int pend2 = -1;
+  [[maybe_unused]] double* const gA = GJR ? Jm + BigWs<NMAX>::OFF_G : nullptr;
   auto compute_d_z = [&](int iq) {
     {
       if constexpr (GJR && (QPGPU_WAVE_TOLLOOP & 1) && S == 4 * 64 && NMAX <= S) {
@@ -793,7 +804,56 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
             for (int u = 0; u < kDC; u++) jv[u] = (row && c0 + u < cA) ? J_(ls, c0 + u) : 0.0;
             chunk(jv, [&](int u) { return c0 + u < cA ? c0 + u : -1; });
           }
-          if (ps >= 0) {
+          if (kDefer2 && ps >= 0 && pend2 >= 0) {
+            // A (coefficients in gA, rotations g = 0..ngA-1 on columns (n-2-g, n-1-g)) then B
+            // (gc, pend2 = ps + 1, one rotation fewer): A's rotation g yields column n-1-g, which
+            // is the t1 of B's rotation g-1 (g = 0: B's initial carry); B's rotation g-1 yields
+            // the final column n-g.  The final columns are written back and both are cleared.
+            const int ngA = n - 1 - ps;
+            double carA = row ? J_(ls, n - 1) : 0.0, carB = 0.0;
+            for (int gb = 0; gb < ngA; gb += kDC) {
+              double t1v[kDC], fv[kDC];
+#pragma unroll
+              for (int u = 0; u < kDC; u++) t1v[u] = (row && gb + u < ngA) ? J_(ls, n - 2 - gb - u) : 0.0;
+#pragma unroll
+              for (int u = 0; u < kDC; u++) {
+                const int g = gb + u;
+                fv[u] = 0.0;
+                if (g < ngA) {
+                  const double c = gA[4 * g], sn = gA[4 * g + 1], xn = gA[4 * g + 2];
+                  const bool f = gA[4 * g + 3] != 0.0;
+                  const double t1 = t1v[u], t2 = carA;
+                  const double n1 = t1 * c + t2 * sn;
+                  const double eA = f ? xn * (t1 + n1) - t2 : t2;  // column n-1-g after A
+                  carA = f ? n1 : t1;
+                  if (g == 0) {
+                    carB = eA;
+                  } else {
+                    const int h = g - 1;
+                    const double cb = GC_(h), sb_ = GS_(h), xb = GX_(h);
+                    const bool fb = GF_(h) != 0.0;
+                    const double n2 = eA * cb + carB * sb_;
+                    fv[u] = fb ? xb * (eA + n2) - carB : carB;  // final column n-g
+                    carB = fb ? n2 : eA;
+                    if (row) J_(ls, n - g) = fv[u];
+                  }
+                }
+              }
+              chunk(fv, [&](int u) { return (gb + u >= 1 && gb + u < ngA) ? n - gb - u : -1; });
+            }
+            if (row) {
+              J_(ls, ps + 1) = carB;
+              J_(ls, ps) = carA;
+            }
+            double cv[kDC];
+#pragma unroll
+            for (int u = 0; u < kDC; u++) cv[u] = u == 0 ? carB : (u == 1 ? carA : 0.0);
+            chunk(cv, [&](int u) { return u == 0 ? ps + 1 : (u == 1 ? ps : -1); });
+            pend = pend2 = -1;
+          } else if (ps >= 0) {
+            // one pending sweep: applied in registers; with two-deep deferral it stays pending
+            // (J is not written back), otherwise its final columns are written now
+            const bool keep = kDefer2;
             const int ng = ctl->ngiv;  // = n - 1 - ps
             double carry = row ? J_(ls, n - 1) : 0.0;
             for (int gb = 0; gb < ng; gb += kDC) {
@@ -811,17 +871,17 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
                   const double n1 = t1 * c + t2 * sn;
                   fv[u] = f ? xn * (t1 + n1) - t2 : t2;
                   carry = f ? n1 : t1;
-                  if (row) J_(ls, n - 1 - g) = fv[u];
+                  if (row && !keep) J_(ls, n - 1 - g) = fv[u];
                 }
               }
               chunk(fv, [&](int u) { return gb + u < ng ? n - 1 - gb - u : -1; });
             }
-            if (row) J_(ls, ps) = carry;
+            if (row && !keep) J_(ls, ps) = carry;
             double cv[kDC];
 #pragma unroll
             for (int u = 0; u < kDC; u++) cv[u] = u == 0 ? carry : 0.0;
             chunk(cv, [&](int u) { return u == 0 ? ps : -1; });
-            pend = -1;
+            if (!keep) pend = -1;
           }
           if (row) zv[ls] = z;
           grp_sync<S>();
@@ -1117,8 +1177,33 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
       return false;
     }
   };
+  // J's trailing columns swept in memory by a recorded set of rotations (coef: 4 per rotation,
+  // as gc) — plain_sweep's arithmetic with the coefficients taken from `coef`
+  [[maybe_unused]] auto sweep_coef = [&](const double* coef, int ng) {
+    for (int k = ls; k < n; k += S) {
+      double carry = J_(k, n - 1);
+      for (int g = 0; g < ng; g++) {
+        const double t1 = J_(k, n - 2 - g), t2 = carry;
+        const double c = coef[4 * g], sn = coef[4 * g + 1], xn = coef[4 * g + 2];
+        const bool f = coef[4 * g + 3] != 0.0;
+        const double n1 = t1 * c + t2 * sn;
+        J_(k, n - 1 - g) = f ? xn * (t1 + n1) - t2 : t2;
+        carry = f ? n1 : t1;
+      }
+      J_(k, n - 1 - ng) = carry;
+    }
+  };
   auto add_constraint = [&]() {
     const uint64_t h0 = clk();
+    if constexpr (kDefer2) {
+      // a sweep is pending (its coefficients in gc): they move to the workspace before this
+      // add's rotations are recorded in gc
+      if (pend >= 0) {
+        const int ngA = n - 1 - pend;
+        for (int e = ls; e < 4 * ngA; e += S) gA[e] = gc[e];
+        grp_sync<S>();
+      }
+    }
     const bool hp = h_prefix(ctl->iq);
     if (lead && !hp) {
       const int iq = ctl->iq;
@@ -1331,8 +1416,18 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
     grp_sync<S>();
     if (defer && iq0 < n) {
       if (ctl->fin) {
-        pend = iq0;
+        if (kDefer2 && pend >= 0)
+          pend2 = iq0;  // = pend + 1: the d/z pass applies both and writes J back
+        else
+          pend = iq0;
       } else {
+        // degenerate: delete_constraint needs the current J — the pending sweep (its
+        // coefficients now in gA), then this one
+        if (kDefer2 && pend >= 0) {
+          sweep_coef(gA, n - 1 - pend);
+          grp_sync<S>();
+          pend = -1;
+        }
         plain_sweep();
         grp_sync<S>();
       }
@@ -1343,6 +1438,15 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
   // R re-triangularisation (recording the rotations), the lanes shift R's rows and rotate
   // J's columns.
   auto delete_constraint = [&](int l) {
+    if constexpr (kDefer2) {
+      // J must be current: a sweep kept pending by the last d/z pass (its coefficients still in
+      // gc: no add since) is applied now
+      if (pend >= 0) {
+        sweep_coef(gc, n - 1 - pend);
+        grp_sync<S>();
+        pend = -1;
+      }
+    }
     if (lead) {
       const int iq = ctl->iq;
       int qq = 0;
