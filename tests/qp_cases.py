@@ -92,3 +92,79 @@ def edge_cases():
                                          np.array([[[1., 0., 1.], [0., 1., 1.]]]), np.array([[1., 1., 1.]]),
                                          np.zeros((1, 2, 0)), np.zeros((1, 0)))))
     return out
+
+
+# ---- seeded fuzz cases (tests/test_gpu_fuzz.py): random shapes across every kernel family and
+# per-QP data modes the configs above do not reach — exact ties in the most-violated selection
+# (small-integer data), ill-conditioned and badly scaled G, zero / duplicated / contradictory
+# constraint columns, rank-deficient CE.  Every QP is drawn from (seed, its index) only.
+
+FUZZ_MODES = ("plain", "ill_conditioned", "scaled", "dup_zero_cols", "contradictory", "rank_def_ce",
+              "diag_box", "integer_ties")
+
+
+def _fuzz_qp(rng, n, p, m, mode, mild):
+    A = rng.standard_normal((n, n))
+    G = A.T @ A + n * np.eye(n)
+    g0 = 10.0 * rng.standard_normal(n)
+    xf = 0.1 * rng.standard_normal(n)
+    CE = rng.standard_normal((n, p))
+    CI = rng.standard_normal((n, m))
+    slack = np.abs(rng.standard_normal(m))
+    if mode == "ill_conditioned":
+        Q, _ = np.linalg.qr(rng.standard_normal((n, n)))
+        k = rng.uniform(1.0, 2.0 if mild else 8.0)
+        G = (Q * np.logspace(0.0, -k, n)) @ Q.T
+        G = 0.5 * (G + G.T)
+    elif mode == "scaled":
+        s = rng.uniform(-3, 3) if mild else rng.uniform(-40, 40)
+        G *= 10.0 ** s
+        g0 *= 10.0 ** (s + rng.uniform(-2, 2))
+        CI *= 10.0 ** rng.uniform(-3 if mild else -20, 3 if mild else 20)
+    elif mode == "dup_zero_cols" and m >= 2:
+        for j in rng.choice(m, size=max(1, m // 3), replace=False):
+            src = int(rng.integers(m))
+            r = int(rng.integers(3))
+            CI[:, j] = CI[:, src] * (1.0 if r == 0 else rng.uniform(0.5, 2.0)) if r < 2 else 0.0
+    elif mode == "diag_box":
+        G = np.diag(rng.uniform(0.1, 10.0, n))
+        if m >= 2 * n:
+            CI[:, :2 * n] = np.hstack([-np.eye(n), np.eye(n)])
+    elif mode == "integer_ties":
+        G = np.diag(rng.integers(1, 4, n).astype(float))
+        g0 = rng.integers(-4, 5, n).astype(float)
+        CE = rng.integers(-1, 2, (n, p)).astype(float)
+        CI = rng.integers(-1, 2, (n, m)).astype(float)
+        xf = np.zeros(n)
+        slack = rng.integers(0, 3, m).astype(float)
+    elif mode == "rank_def_ce" and p >= 2:
+        CE[:, -1] = CE[:, 0] * rng.choice([1.0, -2.0, 0.5])
+    ce0 = -CE.T @ xf
+    ci0 = -CI.T @ xf + slack
+    if mode == "contradictory" and m >= 2:
+        j = int(rng.integers(m - 1))
+        CI[:, j + 1] = -CI[:, j]
+        ci0[j + 1] = -ci0[j] - rng.uniform(0.0, 1.0)
+    if mode == "dup_zero_cols":
+        zero = ~CI.any(axis=0)
+        ci0[zero] = np.where(rng.random(int(zero.sum())) < 0.5, -1.0, 1.0)
+    return G, g0, CE, ce0, CI, ci0
+
+
+def fuzz_case(seed, mild=False):
+    """A batch of random shape: n in [1, 64], p in [0, n], m in [0, 4n] (capped at 256), 1..300
+    QPs, each QP's data mode drawn independently.  mild=True keeps cond(G) <= 1e2 and
+    scales within 1e+-6 (the fast builds' 1e-10 contract is relative to a well-posed problem).
+    Returns (problems, each QP's mode)."""
+    rng = np.random.default_rng([20261018, seed])
+    n = int(rng.choice([int(rng.integers(1, 9)), int(rng.integers(9, 17)), int(rng.integers(17, 65))],
+                       p=[0.5, 0.3, 0.2]))
+    p = int(rng.integers(0, min(n, 10) + 1))
+    m = int(min(256, rng.integers(0, 4 * n + 1)))
+    if n <= 8 and rng.random() < 0.5:
+        m = min(m, 16)
+    B = int(rng.integers(1, 301 if n <= 16 else 65))
+    modes = [FUZZ_MODES[int(rng.integers(len(FUZZ_MODES)))] for _ in range(B)]
+    qs = [_fuzz_qp(np.random.default_rng([20261018, seed, b]), n, p, m, modes[b], mild) for b in range(B)]
+    st = lambda k: np.ascontiguousarray(np.stack([q[k] for q in qs]))
+    return qpgpu.Problems(n, p, m, st(0), st(1), st(2), st(3), st(4), st(5)), modes

@@ -102,3 +102,21 @@ def test_max_steps_cap():
     pr = dict(qp_cases.edge_cases())["long_paths"]
     x, f, st, it = oracle.solve_batch(pr, max_steps=1)
     assert (st == qpgpu.QP_MAX_ITER).any()
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_oracle_fuzz_kkt(seed):
+    """The oracle on the fuzz generator's mild cases (tests/test_gpu_fuzz.py): every QP it calls
+    solved carries an independent KKT certificate, except on rank-deficient CE: there the
+    reference's dependence test (|d_iq| <= eps R_norm: add_constraint @.text+0x21fd of the
+    archive, oracle/qp_oracle.c qpo_add_constraint) can miss a column
+    that is dependent only up to rounding, and it goes on with a near-singular R, as the oracle
+    does.  No generator mode yields a non-positive-definite G."""
+    pr, modes = qp_cases.fuzz_case(seed, mild=True)
+    G0 = pr.G.copy()
+    x, f, st, it = oracle.solve_batch(pr, max_steps=1000 + 100 * (pr.n + pr.p + pr.m))
+    for b in [b for b in np.where(st == qpgpu.QP_OK)[0] if modes[b] != "rank_def_ce"][:40]:
+        stat, eq, ineq = kkt_residual(G0[b], pr.g0[b], pr.CE[b], pr.ce0[b], pr.CI[b], pr.ci0[b], x[b])
+        sc = 1.0 + np.abs(pr.ci0[b]).max(initial=0.0) + np.abs(pr.ce0[b]).max(initial=0.0)
+        assert stat < 1e-7 and eq < 1e-8 * sc and ineq < 1e-8 * sc, (b, stat, eq, ineq)
+    assert not (st == qpgpu.QP_NOT_POSITIVE_DEFINITE).any()
