@@ -151,20 +151,27 @@ def _fuzz_qp(rng, n, p, m, mode, mild):
     return G, g0, CE, ce0, CI, ci0
 
 
-def fuzz_case(seed, mild=False):
+def fuzz_case(seed, mild=False, large=False):
     """A batch of random shape: n in [1, 64], p in [0, n], m in [0, 4n] (capped at 256), 1..300
     QPs, each QP's data mode drawn independently.  mild=True keeps cond(G) <= 1e2 and
     scales within 1e+-6 (the fast builds' 1e-10 contract is relative to a well-posed problem).
+    large=True draws n in [65, 192], m in [0, 2n], 1..4 QPs (the workspace variant's shapes).
     Returns (problems, each QP's mode)."""
-    rng = np.random.default_rng([20261018, seed])
-    n = int(rng.choice([int(rng.integers(1, 9)), int(rng.integers(9, 17)), int(rng.integers(17, 65))],
-                       p=[0.5, 0.3, 0.2]))
-    p = int(rng.integers(0, min(n, 10) + 1))
-    m = int(min(256, rng.integers(0, 4 * n + 1)))
-    if n <= 8 and rng.random() < 0.5:
-        m = min(m, 16)
-    B = int(rng.integers(1, 301 if n <= 16 else 65))
+    rng = np.random.default_rng([20261018 + large, seed])
+    if large:
+        n = int(rng.integers(65, 193))
+        p = int(rng.integers(0, 11))
+        m = int(rng.integers(0, 2 * n + 1))
+        B = int(rng.integers(1, 5))
+    else:
+        n = int(rng.choice([int(rng.integers(1, 9)), int(rng.integers(9, 17)), int(rng.integers(17, 65))],
+                           p=[0.5, 0.3, 0.2]))
+        p = int(rng.integers(0, min(n, 10) + 1))
+        m = int(min(256, rng.integers(0, 4 * n + 1)))
+        if n <= 8 and rng.random() < 0.5:
+            m = min(m, 16)
+        B = int(rng.integers(1, 301 if n <= 16 else 65))
     modes = [FUZZ_MODES[int(rng.integers(len(FUZZ_MODES)))] for _ in range(B)]
-    qs = [_fuzz_qp(np.random.default_rng([20261018, seed, b]), n, p, m, modes[b], mild) for b in range(B)]
+    qs = [_fuzz_qp(np.random.default_rng([20261018 + large, seed, b]), n, p, m, modes[b], mild) for b in range(B)]
     st = lambda k: np.ascontiguousarray(np.stack([q[k] for q in qs]))
     return qpgpu.Problems(n, p, m, st(0), st(1), st(2), st(3), st(4), st(5)), modes

@@ -40,14 +40,19 @@ def test_fuzz_fast(gpu, seed):
     the solve continues with a near-singular R: the reference's x there carries no KKT
     certificate (tests/test_oracle.py::test_oracle_fuzz_kkt), and another rounding lands
     elsewhere.  Those QPs are held bitwise by the default path (test_fuzz_parity) only."""
+    pr, modes = qp_cases.fuzz_case(seed, mild=True)
+    assert_tolerance_contract(pr, modes, f"fast fuzz {seed} {(pr.n, pr.p, pr.m, pr.batch)}", fast=True,
+                              layout="tiled64" if seed % 2 else "qp_major")
+
+
+def assert_tolerance_contract(pr, modes, label, **kw):
+    """The documented contract of the non-bitwise arithmetic (test_fuzz_fast's docstring)."""
     import oracle
     import qpgpu
 
-    pr, modes = qp_cases.fuzz_case(seed, mild=True)
-    label = f"fast fuzz {seed} {(pr.n, pr.p, pr.m, pr.batch)}"
     prc = qpgpu.Problems(pr.n, pr.p, pr.m, pr.G.copy(), pr.g0, pr.CE, pr.ce0, pr.CI, pr.ci0)
     xo, fo, so, io = oracle.solve_batch(prc, max_steps=1000 + 100 * (pr.n + pr.p + pr.m))
-    xg, fg, sg, ig = qpgpu.solve_batched_host(pr, fast=True, layout="tiled64" if seed % 2 else "qp_major")
+    xg, fg, sg, ig = qpgpu.solve_batched_host(pr, **kw)
     held = np.array([md != "rank_def_ce" for md in modes])
     assert np.array_equal(so[held], sg[held]), f"{label}: status differs at {np.where(held & (so != sg))[0]}"
     assert np.array_equal(io[held], ig[held]), f"{label}: l1 passes differ at {np.where(held & (io != ig))[0]}"
@@ -61,3 +66,21 @@ def test_fuzz_fast(gpu, seed):
     f_unc = np.abs([g @ np.linalg.solve(G, g) for G, g in zip(pr.G[ok], pr.g0[ok])])
     badf = np.where(df > TOL * fs + X_FLOOR * (1.0 + f_unc))[0]
     assert not badf.size, f"{label}: f off at {np.where(ok)[0][badf]}: {df[badf]} vs terms {fs[badf]}"
+
+
+# ---- n in [65, 192]: the workspace variant.  QPGPU_FLAG_EXACT keeps the reference's
+# order (bitwise on every mode); the default there is the tolerance mode (MFMA panel setup, tree
+# sums), held to the same contract as the fast builds on the mild cases.
+
+@pytest.mark.parametrize("seed", range(16))
+def test_fuzz_large_exact(gpu, seed):
+    pr, _ = qp_cases.fuzz_case(seed, large=True)
+    assert_parity(pr, f"large fuzz {seed} {(pr.n, pr.p, pr.m, pr.batch)}", exact=True,
+                  write_factor=seed % 4 == 0, layout="tiled64" if seed % 2 else "qp_major")
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_fuzz_large_default(gpu, seed):
+    pr, modes = qp_cases.fuzz_case(seed, mild=True, large=True)
+    assert_tolerance_contract(pr, modes, f"large fuzz default {seed} {(pr.n, pr.p, pr.m, pr.batch)}",
+                              layout="tiled64" if seed % 2 else "qp_major")
