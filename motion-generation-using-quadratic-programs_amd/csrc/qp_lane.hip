@@ -46,8 +46,9 @@
 #define QPK_LANE_C(name) name
 #endif
 
-// Diagnostic s_memtime stamps (tools/stamps.py): compiled in only when QPGPU_LANE_STAMPS is 1
-// (A/B builds); the product build carries none of their SGPR state.
+// Diagnostic s_memtime stamps (tools/stamps.py): compiled in (QPGPU_LANE_STAMPS = 1), each one a
+// wave-uniform null test of a.stamps unless a stamp buffer is passed; 0 removes them (measured
+// the same C1 time either way, profiles/r05_s8), 2 adds the loop's l2a split.
 #ifndef QPGPU_LANE_STAMPS
 #define QPGPU_LANE_STAMPS 1
 #endif
