@@ -90,7 +90,10 @@ thread_local HostWorkspace g_ws;
 
 // Device workspace for the kernels that keep J and R in global memory (n > 64).  Grow-only and
 // cached per (device, stream), so launches on different streams never share one; growing syncs
-// only the stream that used the old buffer.
+// only the stream that used the old buffer.  The caller keeps `hold` (the cache's lock) until its
+// launches are enqueued: a host thread that grows the buffer of a stream another thread has just
+// been handed — the default stream, say — would otherwise free it before that thread's kernel is
+// in the stream (the stream sync before the free only covers work already enqueued).
 struct DevWorkspace {
   void* buf = nullptr;
   size_t bytes = 0;
@@ -98,13 +101,13 @@ struct DevWorkspace {
 std::mutex g_dev_ws_mu;
 std::map<std::pair<int, hipStream_t>, DevWorkspace> g_dev_ws;
 
-int device_workspace(int64_t bytes, hipStream_t stream, double** out) {
+int device_workspace(int64_t bytes, hipStream_t stream, double** out, std::unique_lock<std::mutex>& hold) {
   *out = nullptr;
   if (bytes <= 0) return QPGPU_SUCCESS;
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
-  std::lock_guard<std::mutex> lk(g_dev_ws_mu);
+  if (!hold.owns_lock()) hold = std::unique_lock<std::mutex>(g_dev_ws_mu);
   DevWorkspace& w = g_dev_ws[{dev, stream}];
   if (w.bytes < (size_t)bytes) {
     if (w.buf) {
@@ -251,6 +254,7 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int handled = 0;
   hipError_t e = hipSuccess;
+  std::unique_lock<std::mutex> ws_hold;  // the workspace cache's lock, once a workspace is taken
   a.flags = d->flags & (QPGPU_FLAG_WRITE_FACTOR | QPGPU_FLAG_EXACT);
   const bool fast = (d->flags & QPGPU_FLAG_FAST) != 0;
   auto launch_lane = [&]() {
@@ -264,7 +268,7 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
       if (handled) return QPGPU_SUCCESS;
     }
     double* ws = nullptr;
-    const int wrc = device_workspace(qpk_medium_workspace_bytes(a.n, a.m, a.batch), s, &ws);
+    const int wrc = device_workspace(qpk_medium_workspace_bytes(a.n, a.m, a.batch), s, &ws, ws_hold);
     if (wrc) return wrc;
     e = qpk_launch_medium_ws(&a, s, &handled, nullptr, ws);
     return QPGPU_SUCCESS;
@@ -284,7 +288,7 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
       if (chunk < (a.tile == 64 ? 64 : 1)) chunk = a.tile == 64 ? 64 : 1;
     }
     double* ws = nullptr;
-    const int wrc = device_workspace(per * (chunk < a.batch ? chunk : a.batch), s, &ws);
+    const int wrc = device_workspace(per * (chunk < a.batch ? chunk : a.batch), s, &ws, ws_hold);
     if (wrc) return wrc;
     handled = 1;
     const int64_t n = a.n, p = a.p, m = a.m;

@@ -222,6 +222,45 @@ def test_device_api_matches_host_api(gpu):
     assert np.array_equal(db.G.cpu().numpy(), pr.G)
 
 
+def test_threads_share_one_stream_workspace(gpu):
+    """Host threads enqueueing workspace-kernel solves (n > 64) of different sizes on the SAME
+    stream (the device's default stream): the grow-only workspace cached per (device, stream)
+    must not be freed under a launch another thread has not enqueued yet (qpgpu_api.cpp
+    device_workspace holds its lock through the enqueue).  Every thread's batch stays bitwise
+    equal to the oracle (EXACT)."""
+    import threading
+
+    import torch
+
+    shapes = [(66, 2, 80, 3), (120, 4, 200, 2), (90, 0, 150, 4), (160, 3, 240, 2)]
+    cases = []
+    for k, (n, p, m, B) in enumerate(shapes):
+        pr = qpgpu.make_problems("general", n, p, m, 0, B, seed=500 + k)
+        prc = qpgpu.Problems(n, p, m, pr.G.copy(), pr.g0, pr.CE, pr.ce0, pr.CI, pr.ci0)
+        cases.append((qpgpu.DeviceBatch(pr, "cuda:0"), oracle.solve_batch(prc)))
+    s = torch.cuda.default_stream(torch.device("cuda:0"))
+    errors = []
+
+    def worker(db, reps):
+        try:
+            for _ in range(reps):
+                db.solve(stream=s, exact=True)
+        except Exception as exc:  # surfaced in the main thread
+            errors.append(exc)
+
+    threads = [threading.Thread(target=worker, args=(db, 6)) for db, _ in cases]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+    for (db, (xo, fo, so, io)), (n, p, m, B) in zip(cases, shapes):
+        x, f, st, it = db.results()
+        assert np.array_equal(st, so) and np.array_equal(it, io), (n, p, m)
+        assert not _bit_mismatch(x, xo) and not _bit_mismatch(f, fo), (n, p, m)
+
+
 def test_python_mirror_raises_like_reference(gpu):
     with pytest.raises(RuntimeError, match="Constraints are linearly dependent"):
         qpgpu.solve_quadprog(2 * np.eye(3), np.ones(3), [[1., 1.], [2., 2.], [0., 0.]], [1., 1.],
