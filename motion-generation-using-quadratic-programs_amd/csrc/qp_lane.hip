@@ -1235,6 +1235,16 @@ __global__ void __launch_bounds__(64, 1) QP_LANE_KERNEL(const QpArgs a) {
   }
 }
 
+// The exact build's p = 0 instantiations (C2, the joint-limit QPs) are compiled in their own
+// translation unit (qp_lane_p0.hip, QPGPU_LANE_PART = 2) under LLVM's iterative-minreg scheduler,
+// the rest (QPGPU_LANE_PART = 1) under iterative-ilp: measured C2 71.2-71.9 -> 68.6-69.1 us with
+// minreg, while C1 is slower with it (43.7-44.7 -> 46.1-47.9 us; profiles/r05_s11).  Part 0 (the
+// fast build, A/B builds) keeps every instantiation in one TU.
+#ifndef QPGPU_LANE_PART
+#define QPGPU_LANE_PART 0
+#endif
+template <int NM, int MM, int T>
+static void launch_lane_p0(const QpArgs& a, hipStream_t stream);
 template <int NM, int MM, int T>
 static void launch_lane_t(const QpArgs& a, hipStream_t stream) {
   const int64_t blocks = (a.batch + kQpw - 1) / kQpw;
@@ -1257,7 +1267,7 @@ static void launch_lane_t(const QpArgs& a, hipStream_t stream) {
     if (a.p == 6)
       hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, 6>), g, blk, 0, stream, a);
     else if (a.p == 0)
-      hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, 0>), g, blk, 0, stream, a);
+      launch_lane_p0<NM, MM, T>(a, stream);
     else
       hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, -1>), g, blk, 0, stream, a);
   } else {
@@ -1265,6 +1275,23 @@ static void launch_lane_t(const QpArgs& a, hipStream_t stream) {
   }
 }
 
+#if QPGPU_LANE_PART == 1
+}  // namespace QPK_LANE_NS
+extern "C" void qpk_launch_lane_p0(const qpk::QpArgs* a, hipStream_t stream);  // qp_lane_p0.hip
+namespace QPK_LANE_NS {
+template <int NM, int MM, int T>
+static void launch_lane_p0(const QpArgs& a, hipStream_t stream) {
+  qpk_launch_lane_p0(&a, stream);
+}
+#else
+template <int NM, int MM, int T>
+static void launch_lane_p0(const QpArgs& a, hipStream_t stream) {
+  const int64_t blocks = (a.batch + kQpw - 1) / kQpw;
+  hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, 0>), dim3((unsigned)blocks), dim3(64), 0, stream, a);
+}
+#endif
+
+#if QPGPU_LANE_PART != 2
 template <int NM, int MM>
 static hipError_t launch_lane(const QpArgs& a, hipStream_t stream) {
   if (a.tile == 64)
@@ -1290,9 +1317,20 @@ const LaneVariant* pick_lane(int n, int m) {
     if (n <= v.nmax && m <= v.mmax) return &v;
   return nullptr;
 }
+#endif  // QPGPU_LANE_PART != 2
 
 }  // namespace QPK_LANE_NS
 
+#if QPGPU_LANE_PART == 2
+// part 2: the exact p = 0 kernels only (the caller, part 1's launch_lane_t, has matched the shape)
+extern "C" void qpk_launch_lane_p0(const qpk::QpArgs* a, hipStream_t stream) {
+  using namespace QPK_LANE_NS;
+  if (a->n == 7 && a->m == 14)
+    a->tile == 64 ? launch_lane_p0<7, 14, 64>(*a, stream) : launch_lane_p0<7, 14, 1>(*a, stream);
+  else if (a->n == 8 && a->m == 16)
+    a->tile == 64 ? launch_lane_p0<8, 16, 64>(*a, stream) : launch_lane_p0<8, 16, 1>(*a, stream);
+}
+#else
 extern "C" hipError_t QPK_LANE_C(qpk_launch_lane)(const qpk::QpArgs* a, hipStream_t stream, int* handled,
                                                   const char** name) {
   const QPK_LANE_NS::LaneVariant* v = QPK_LANE_NS::pick_lane(a->n, a->m);
@@ -1309,3 +1347,4 @@ extern "C" const char* QPK_LANE_C(qpk_lane_name)(int n, int /*p*/, int m) {
   const QPK_LANE_NS::LaneVariant* v = QPK_LANE_NS::pick_lane(n, m);
   return v ? v->name : nullptr;
 }
+#endif  // QPGPU_LANE_PART == 2
