@@ -512,6 +512,27 @@ def test_generic_beyond_specialised_shapes(gpu, kind, n, p, m, B, write_factor):
                   write_factor=write_factor)
 
 
+# every size class's largest shape and the first one past it (kernel_name and the default path):
+# lane (8, 16), subgroup S=8 (8, 32), wave LDS variants (16, 32) / (32, 128) / (64, 256), the
+# workspace variant (256, 1024), then the generic kernel
+BOUNDARY_SHAPES = [(8, 2, 16, 130), (8, 2, 17, 130), (9, 2, 16, 130), (8, 0, 32, 70), (8, 0, 33, 70),
+                   (16, 3, 32, 40), (17, 3, 32, 40), (32, 4, 128, 20), (33, 4, 128, 20),
+                   (64, 5, 256, 6), (65, 5, 256, 4), (256, 4, 1024, 1), (256, 4, 1025, 1),
+                   (257, 4, 1024, 1)]
+
+
+@pytest.mark.parametrize("n,p,m,B", BOUNDARY_SHAPES)
+def test_size_class_boundaries(gpu, n, p, m, B):
+    """Each kernel family's largest shape and the first shape past it, on the default path:
+    bitwise against the oracle where the path keeps the reference's order, within 1e-10 with
+    identical status and passes in the n > 64 tolerance mode, and EXACT bitwise everywhere."""
+    pr = qp_cases.make("general", n, p, m, B, seed=n * 1000 + m)
+    assert qpgpu.kernel_name(n, p, m), (n, p, m)
+    assert_parity(pr, f"boundary {(n, p, m)} [{qpgpu.kernel_name(n, p, m)}]")
+    if not bitwise_expected(n, m):
+        assert_parity(pr, f"boundary {(n, p, m)} EXACT", exact=True)
+
+
 @pytest.mark.parametrize("layout,B", [("qp_major", 10), ("tiled64", 150)])
 def test_generic_sub_batches(gpu, layout, B):
     """The generic kernel over sub-batches (its per-launch workspace capped, qpgpu_api.cpp): with
