@@ -146,7 +146,9 @@ typedef struct qpgpu_problem_desc {
  * The call only enqueues work and does not synchronise, so it can be captured into a hipGraph.
  * Shapes with n > 64 (J and R in global memory) use a device workspace cached per
  * (device, stream): the first call on a stream allocates it (do that before capturing), and
- * launches on different streams never share one.  G is read-only unless
+ * launches on different streams never share one.  Host threads may call concurrently, on one
+ * stream or several: the workspace cache's lock is held until a call's launches are enqueued, so
+ * launches on one stream share its workspace in stream order.  G is read-only unless
  * QPGPU_FLAG_WRITE_FACTOR is set.
  * `iters` (l1 passes per QP, the reference's `iter`) may be NULL.
  * Replaces: the per-QP call at reference src/mgqp.cpp:708, batched. */
@@ -174,6 +176,7 @@ int qpgpu_solve_batched_eq(const qpgpu_problem_desc* d,
 /* Same, with HOST pointers: copies the inputs to the device, solves, copies the outputs back
  * and synchronises.  This is what the ArrayHH drop-in (libquadprog_amd.so) calls for each
  * solve_quadprog(); it always runs the HIP kernel (there is no CPU path in the product).
+ * Each host thread has its own device buffers, pinned staging buffer and stream.
  * G receives the Cholesky factor when QPGPU_FLAG_WRITE_FACTOR is set. */
 int qpgpu_solve_batched_host(const qpgpu_problem_desc* d,
                              double* G, const double* g0,
