@@ -60,13 +60,13 @@ def _worker(rank, world, port, per_rank, steps, slots, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("steps,slots", [(1, 1), (5, 3)])
-def test_two_rank_pipelined_gather(tmp_path, steps, slots):
+@pytest.mark.parametrize("world,steps,slots", [(2, 1, 1), (2, 5, 3), (4, 3, 2)])
+def test_multi_rank_pipelined_gather(tmp_path, world, steps, slots):
     sys.path[:0] = [PKG, os.path.join(ROOT, "oracle")]
     import oracle
     import qpgpu
 
-    per_rank, world = 200, 2
+    per_rank = 200
     out = str(tmp_path / "gathered.npz")
     mp.start_processes(_worker, args=(world, _free_port(), per_rank, steps, slots, out),
                        nprocs=world, join=True, start_method="spawn")
