@@ -84,3 +84,37 @@ def test_fuzz_large_default(gpu, seed):
     pr, modes = qp_cases.fuzz_case(seed, mild=True, large=True)
     assert_tolerance_contract(pr, modes, f"large fuzz default {seed} {(pr.n, pr.p, pr.m, pr.batch)}",
                               layout="tiled64" if seed % 2 else "qp_major")
+
+
+@pytest.mark.parametrize("seed", range(0, 48, 3))
+def test_fuzz_single_calls(gpu, seed):
+    """The reference's own call pattern — one solve_quadprog() per QP — through the Python mirror
+    of the drop-in (qpgpu.solve_quadprog: the host entry's pinned staging, one H2D, the kernel,
+    one D2H): the first QPs of each fuzz case, bitwise against the oracle's single solve (x, f
+    and the factor left in G), and the reference's exceptions where it throws."""
+    import oracle
+    import qpgpu
+
+    pr, modes = qp_cases.fuzz_case(seed)
+    for b in range(min(pr.batch, 12)):
+        G = pr.G[b].copy()
+        Go = pr.G[b].copy()
+        st, fo, xo, _ = oracle.solve_one(Go, pr.g0[b], pr.CE[b], pr.ce0[b], pr.CI[b], pr.ci0[b],
+                                         max_steps=1000 + 100 * (pr.n + pr.p + pr.m))  # the C-ABI's cap
+        label = f"seed {seed} qp {b} ({modes[b]})"
+        if st == qpgpu.QP_NOT_POSITIVE_DEFINITE:
+            with pytest.raises(ValueError, match="cholesky"):
+                qpgpu.solve_quadprog(G, pr.g0[b], pr.CE[b], pr.ce0[b], pr.CI[b], pr.ci0[b])
+            continue
+        if st == qpgpu.QP_MAX_ITER:  # (the reference has no cap; the mirror raises at it)
+            with pytest.raises(RuntimeError, match="step cap"):
+                qpgpu.solve_quadprog(G, pr.g0[b], pr.CE[b], pr.ce0[b], pr.CI[b], pr.ci0[b])
+            continue
+        if st == qpgpu.QP_DEPENDENT:
+            with pytest.raises(RuntimeError, match="linearly dependent"):
+                qpgpu.solve_quadprog(G, pr.g0[b], pr.CE[b], pr.ce0[b], pr.CI[b], pr.ci0[b])
+            continue
+        f, x = qpgpu.solve_quadprog(G, pr.g0[b], pr.CE[b], pr.ce0[b], pr.CI[b], pr.ci0[b])
+        assert np.float64(f).view(np.uint64) == np.float64(fo).view(np.uint64) or (np.isnan(f) and np.isnan(fo)), label
+        assert np.array_equal(np.asarray(x).view(np.uint64), np.asarray(xo).view(np.uint64)), label
+        assert np.array_equal(G.view(np.uint64), Go.view(np.uint64)), label
