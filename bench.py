@@ -27,8 +27,8 @@ Timing: steps are independent batches, pipelined round-robin over --streams HIP 
 steps serialized on one stream.  `roofline` uses the kernel's own duration: --kernel-reps
 serialized launches on one stream between one HIP-event pair on that stream (cold rotation;
 the launch-to-launch average, which includes the dependent-launch gap and sits just above what
-`rocprofv3 --kernel-trace --stats -- python bench.py --streams 1` reports per kernel); the
-average of one event pair per launch is reported beside it.
+`rocprofv3 --kernel-trace --stats -- python bench.py --streams 1` reports per kernel), the median
+of --kernel-rounds such rounds; the average of one event pair per launch is reported beside it.
 
 Single-GPU:  python bench.py [--steps K --warmup W] [--config C1|C2|C3|C4|mgqp|C5]
 Multi-GPU:   python bench.py --gpus N ...   (starts torch.distributed.run with N ranks itself)
@@ -108,6 +108,8 @@ def parse(argv=None):
                          "defeat the Infinity Cache, 1 = warm)")
     ap.add_argument("--kernel-reps", type=int, default=20,
                     help="serialized launches timed for the roofline's kernel duration")
+    ap.add_argument("--kernel-rounds", type=int, default=5,
+                    help="rounds of --kernel-reps launches (median round reported)")
     ap.add_argument("--exact", action="store_true",
                     help="the bitwise builds (the reference's operation order; the default)")
     ap.add_argument("--fast", action="store_true",
@@ -447,31 +449,48 @@ def main():
     # that stream around each launch, rotating over the cold sets (and once more warm)
     cs = streams[0]
 
-    def kernel_ms(rotate, per_launch=False, fast=None, family=None):
+    kernel_rounds = {}
+
+    def kernel_ms(rotate, per_launch=False, fast=None, family=None, key=None):
         # one HIP-event pair around kernel_reps back-to-back launches on one stream (average
-        # launch-to-launch duration: kernel + the dependent-launch gap), or a pair per launch
+        # launch-to-launch duration: kernel + the dependent-launch gap), or a pair per launch.
+        # 3 x kernel_reps untimed launches bring the GPU out of its idle clocks (the bench syncs
+        # before this), then --kernel-rounds rounds, each after 5 more untimed launches; the
+        # median round is the figure and every round is reported (one 20-launch round spans
+        # < 1 ms: a single round right after a sync moved with the clock ramp, 44.6-48.0 us for
+        # the same C1 kernel, profiles/r05_f2-f4; later rounds of one run were faster, r05_s17)
         K_ = args.kernel_reps
         fns = [launcher(q % R if rotate else 0, 0, cs, fast, family) for q in range(K_)]
-        if per_launch:
-            st_ = [torch.cuda.Event(enable_timing=True) for _ in range(K_)]
-            en_ = [torch.cuda.Event(enable_timing=True) for _ in range(K_)]
-            for q in range(K_):
-                st_[q].record(cs)
+        rounds = []
+        for q in range(3 * K_):  # ~3 x K_ untimed launches first: the clocks ramp over ~1 ms
+            fns[q % K_]()
+        for _ in range(max(1, args.kernel_rounds)):
+            for q in range(min(K_, 5)):
                 fns[q]()
-                en_[q].record(cs)
+            if per_launch:
+                st_ = [torch.cuda.Event(enable_timing=True) for _ in range(K_)]
+                en_ = [torch.cuda.Event(enable_timing=True) for _ in range(K_)]
+                for q in range(K_):
+                    st_[q].record(cs)
+                    fns[q]()
+                    en_[q].record(cs)
+                torch.cuda.synchronize(dev)
+                rounds.append(float(np.mean([a_.elapsed_time(b_) for a_, b_ in zip(st_, en_)])))
+                continue
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cs)
+            for q in range(K_):
+                fns[q]()
+            e1.record(cs)
             torch.cuda.synchronize(dev)
-            return float(np.mean([a_.elapsed_time(b_) for a_, b_ in zip(st_, en_)]))
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(cs)
-        for q in range(K_):
-            fns[q]()
-        e1.record(cs)
-        torch.cuda.synchronize(dev)
-        return e0.elapsed_time(e1) / K_
+            rounds.append(e0.elapsed_time(e1) / K_)
+        if key:
+            kernel_rounds[key] = rounds
+        return float(np.median(rounds))
 
-    kern_cold = kernel_ms(True)
-    kern_warm = kernel_ms(False)
-    kern_cold_pair = kernel_ms(True, per_launch=True)
+    kern_cold = kernel_ms(True, key="cold")
+    kern_warm = kernel_ms(False, key="warm")
+    kern_cold_pair = kernel_ms(True, per_launch=True, key="cold_event_pair_per_launch")
     # the other arithmetic mode of the same shape on the same box, when it has its own kernel
     # (the lane kernel's QPGPU_FLAG_FAST build, n <= 8, m <= 16): kernel time and its agreement
     # with this line's solve of set 0 (status identical; x, f relative error)
@@ -602,9 +621,12 @@ def main():
            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
            "traffic_ratio": (traffic / (bpq * B)) if traffic else None,
            "kernel_ms": kern_cold,
-           "kernel_ms_source": f"{args.kernel_reps} serialized launches on one stream "
-                               "between one HIP-event pair (launch-to-launch average), "
+           "kernel_ms_source": f"median of {max(1, args.kernel_rounds)} rounds of "
+                               f"{args.kernel_reps} serialized launches on one stream between "
+                               "one HIP-event pair (launch-to-launch average), after "
+                               f"{3 * args.kernel_reps} untimed launches and 5 more per round; "
                                f"inputs rotating over {R} resident set(s)",
+           "kernel_ms_rounds": kernel_rounds.get("cold"),
            "kernel_ms_event_pair_per_launch": kern_cold_pair,
            "warm": {"kernel_ms": kern_warm, "achieved": achieved_warm,
                     "frac": achieved_warm / HBM_PEAK_GBS},

@@ -26,6 +26,8 @@
 // failed check re-solves with the IEEE forms.
 #include <climits>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include <type_traits>
 
@@ -2067,13 +2069,22 @@ static hipError_t launch_wave(const QpArgs& a, hipStream_t stream, double* ws) {
     const size_t want = (size_t)163840 / cap - 1024;
     if (want > lds_bytes) lds_bytes = want;
   }
-  static size_t granted = 0;  // dynamic LDS beyond 64 KiB must be granted per kernel
-  if (lds_bytes > 65536 && lds_bytes > granted) {
-    const hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&QP_WAVE_KERNEL<S, NMAX, MMAX, GJR>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  // dynamic LDS beyond 64 KiB must be granted per kernel and device; host threads may launch
+  // concurrently (include/qpgpu.h), so the record of what was granted is locked
+  if (lds_bytes > 65536) {
+    static std::mutex mu;
+    static std::map<int, size_t> granted;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    granted = lds_bytes;
+    std::lock_guard<std::mutex> lk(mu);
+    size_t& g = granted[dev];
+    if (lds_bytes > g) {
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&QP_WAVE_KERNEL<S, NMAX, MMAX, GJR>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+      if (e != hipSuccess) return e;
+      g = lds_bytes;
+    }
   }
   hipLaunchKernelGGL((QP_WAVE_KERNEL<S, NMAX, MMAX, GJR>), dim3((unsigned)blocks), dim3(C::BS), lds_bytes,
                      stream, a, ws);
