@@ -53,6 +53,13 @@ MALL_BYTES = 256 << 20  # Infinity Cache
 C4_GLOBAL = 1 << 20
 CPU_THREAD_CAP = 16  # a one-GPU job's CPU share on the box (os.cpu_count() is the whole machine)
 # name: (kind, n, p, m, default batch per GPU (0 = C4 split), description)
+# Default (warmup, timed) steps per config: enough sustained load that the GPU runs at its
+# steady-state clocks in the timed region.  Measured on C1 (profiles/r05_s19, r05_s20): (10, 50)
+# 1.79-1.90e9 solves/s with the kernel at 42.3-42.7 us; (200, 500) 2.01e9 / 40.6 us; (1000, 2000)
+# 2.16-2.17e9 / 40.5-40.8 us — a 1.7 ms timed region caught the clocks still ramping.
+DEFAULT_STEPS = {"C1": (1000, 2000), "C2": (1000, 2000), "C4": (500, 1000), "mgqp": (60, 200),
+                 "C3": (10, 30), "C5": (1, 3)}
+
 CONFIGS = {
     "C1": ("general", 7, 6, 14, 65536, "C1: 65536 x (n=7, p=6, m=14) general QPs per GPU"),
     "C4": ("general", 7, 6, 14, 0, "C4: 1048576 x (n=7, p=6, m=14) general QPs split over the GPUs"),
@@ -86,8 +93,10 @@ def metric_name(cfg, n, p, m, B, world):
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default per config: DEFAULT_STEPS, >= ~60 ms of timed work)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed warmup steps (default per config: DEFAULT_STEPS)")
     ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
                     help="workload (default: C1 on one GPU, C4 on N > 1)")
     ap.add_argument("--batch", type=int, default=0, help="QPs per GPU (default: the config's)")
@@ -110,6 +119,8 @@ def parse(argv=None):
                     help="serialized launches timed for the roofline's kernel duration")
     ap.add_argument("--kernel-rounds", type=int, default=5,
                     help="rounds of --kernel-reps launches (median round reported)")
+    ap.add_argument("--kernel-warmup", type=int, default=-1,
+                    help="untimed launches before the kernel-duration rounds (-1: 3 x --kernel-reps)")
     ap.add_argument("--exact", action="store_true",
                     help="the bitwise builds (the reference's operation order; the default)")
     ap.add_argument("--fast", action="store_true",
@@ -322,6 +333,10 @@ def main():
 
     cfg = args.config or ("C1" if world == 1 else "C4")
     kind, n, p, m, bdef, desc = CONFIGS[cfg]
+    if args.warmup is None:
+        args.warmup = DEFAULT_STEPS[cfg][0]
+    if args.steps is None:
+        args.steps = DEFAULT_STEPS[cfg][1]
     if cfg == "C4" and not args.batch:
         if C4_GLOBAL % world:
             sys.exit(f"C4: {C4_GLOBAL} QPs do not split evenly over {world} ranks")
@@ -462,8 +477,8 @@ def main():
         K_ = args.kernel_reps
         fns = [launcher(q % R if rotate else 0, 0, cs, fast, family) for q in range(K_)]
         rounds = []
-        for q in range(3 * K_):  # ~3 x K_ untimed launches first: the clocks ramp over ~1 ms
-            fns[q % K_]()
+        for q in range(args.kernel_warmup if args.kernel_warmup >= 0 else 3 * K_):
+            fns[q % K_]()  # untimed: the clocks ramp up under sustained load
         for _ in range(max(1, args.kernel_rounds)):
             for q in range(min(K_, 5)):
                 fns[q]()
@@ -624,7 +639,8 @@ def main():
            "kernel_ms_source": f"median of {max(1, args.kernel_rounds)} rounds of "
                                f"{args.kernel_reps} serialized launches on one stream between "
                                "one HIP-event pair (launch-to-launch average), after "
-                               f"{3 * args.kernel_reps} untimed launches and 5 more per round; "
+                               f"{args.kernel_warmup if args.kernel_warmup >= 0 else 3 * args.kernel_reps} "
+                               "untimed launches and 5 more per round; "
                                f"inputs rotating over {R} resident set(s)",
            "kernel_ms_rounds": kernel_rounds.get("cold"),
            "kernel_ms_event_pair_per_launch": kern_cold_pair,
