@@ -23,7 +23,9 @@ while it plus everything touched between two uses fits in ~256 MiB).  The warm f
 re-solved) is reported beside it.
 
 Timing: steps are independent batches, pipelined round-robin over --streams HIP streams (default
-3) with private outputs; `value` is that whole-job throughput.  `value_streams1` is the same K
+3) with private outputs; `value` is that whole-job throughput.  Before the W warmup steps the GPU
+runs untimed solver steps for --prewarm-ms (default 40 ms), so the timed region sees its
+steady-state clocks whatever W and K are.  `value_streams1` is the same K
 steps serialized on one stream.  `roofline` uses the kernel's own duration: --kernel-reps
 serialized launches on one stream between one HIP-event pair on that stream (cold rotation;
 the launch-to-launch average, which includes the dependent-launch gap and sits just above what
@@ -119,8 +121,11 @@ def parse(argv=None):
                     help="serialized launches timed for the roofline's kernel duration")
     ap.add_argument("--kernel-rounds", type=int, default=5,
                     help="rounds of --kernel-reps launches (median round reported)")
+    ap.add_argument("--prewarm-ms", type=float, default=40.0,
+                    help="untimed solver steps for this long before the warmup steps (GPU clocks)")
     ap.add_argument("--kernel-warmup", type=int, default=-1,
-                    help="untimed launches before the kernel-duration rounds (-1: 3 x --kernel-reps)")
+                    help="untimed launches before the kernel-duration rounds (-1: at least "
+                         "3 x --kernel-reps and --prewarm-ms / 2 of wall time)")
     ap.add_argument("--exact", action="store_true",
                     help="the bitwise builds (the reference's operation order; the default)")
     ap.add_argument("--fast", action="store_true",
@@ -425,6 +430,24 @@ def main():
         sync_all()
         return time.perf_counter() - t0
 
+    # bring the GPU to its steady-state clocks before anything is timed, whatever W and K are:
+    # untimed solver steps (no gather) for --prewarm-ms of wall time (round 5 measured a short
+    # run inside the clock ramp: C1 1.88e9 vs 2.21e9 solves/s, profiles/r05_s19-s21)
+    # (at most S + 1 steps in flight, so the wall clock follows the GPU without idling it)
+    t_pw = time.perf_counter()
+    k_pw = 0
+    inflight = []
+    while k_pw == 0 or (time.perf_counter() - t_pw) * 1e3 < args.prewarm_ms:
+        step(k_pw, S)
+        ev = torch.cuda.Event()
+        ev.record(streams[k_pw % S])
+        inflight.append(ev)
+        if len(inflight) > S:
+            inflight.pop(0).synchronize()
+        k_pw += 1
+    sync_all()
+    prewarm = {"steps": k_pw, "ms": round((time.perf_counter() - t_pw) * 1e3, 2),
+               "note": "untimed solver steps before the W warmup steps (steady-state clocks)"}
     elapsed = timed(args.steps, args.warmup, S, args.gather if gat else "none")
     # the last step of every stream slot, checked against set 0's solve rotated (guards the
     # pipelining and the rotated sets): x, f, status bit for bit
@@ -477,8 +500,19 @@ def main():
         K_ = args.kernel_reps
         fns = [launcher(q % R if rotate else 0, 0, cs, fast, family) for q in range(K_)]
         rounds = []
-        for q in range(args.kernel_warmup if args.kernel_warmup >= 0 else 3 * K_):
-            fns[q % K_]()  # untimed: the clocks ramp up under sustained load
+        if args.kernel_warmup >= 0:
+            for q in range(args.kernel_warmup):
+                fns[q % K_]()  # untimed: the clocks ramp up under sustained load
+        else:  # untimed launches for --prewarm-ms / 2 of wall time (at most 4 in flight)
+            t_kw, q, evs = time.perf_counter(), 0, []
+            while q < 3 * K_ or (time.perf_counter() - t_kw) * 2e3 < args.prewarm_ms:
+                fns[q % K_]()
+                ev = torch.cuda.Event()
+                ev.record(cs)
+                evs.append(ev)
+                if len(evs) > 4:
+                    evs.pop(0).synchronize()
+                q += 1
         for _ in range(max(1, args.kernel_rounds)):
             for q in range(min(K_, 5)):
                 fns[q]()
@@ -639,8 +673,9 @@ def main():
            "kernel_ms_source": f"median of {max(1, args.kernel_rounds)} rounds of "
                                f"{args.kernel_reps} serialized launches on one stream between "
                                "one HIP-event pair (launch-to-launch average), after "
-                               f"{args.kernel_warmup if args.kernel_warmup >= 0 else 3 * args.kernel_reps} "
-                               "untimed launches and 5 more per round; "
+                               + (f"{args.kernel_warmup} untimed launches" if args.kernel_warmup >= 0 else
+                                  f"untimed launches for >= {args.prewarm_ms / 2:g} ms (and >= {3 * args.kernel_reps})")
+                               + " and 5 more per round; "
                                f"inputs rotating over {R} resident set(s)",
            "kernel_ms_rounds": kernel_rounds.get("cold"),
            "kernel_ms_event_pair_per_launch": kern_cold_pair,
@@ -678,6 +713,7 @@ def main():
         "unit": "QP solves/s",
         "n_gpus": world,
         "steps": args.steps,
+        "prewarm": prewarm,
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "higher_is_better": True,
