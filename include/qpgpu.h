@@ -184,6 +184,22 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d,
                              const double* CI, const double* ci0,
                              double* x, double* f, int32_t* status, int32_t* iters);
 
+/* Same as qpgpu_solve_batched_host, over several GPUs of one node from one host process: the
+ * batch is split into `ndev` contiguous shards (shard k = QPs [k*B/ndev, (k+1)*B/ndev), rounded
+ * to whole 64-QP tiles in the TILED64 layout), shard k is solved on device devices[k] by a
+ * worker thread of its own (its own device buffers and stream, kept across calls), and each
+ * shard's x, f, status, iters (and the factor in G with QPGPU_FLAG_WRITE_FACTOR) land in the
+ * caller's buffers at the shard's offset — the gather of SURVEY §8(e) into host memory.  A device
+ * may be listed more than once (its shards then run concurrently on separate streams).
+ * Returns when every shard is done: the first failing shard's code, or QPGPU_SUCCESS.  Results
+ * are identical to one qpgpu_solve_batched_host call on the whole batch.  ndev <= 64.
+ * Replaces: the per-QP call at reference src/mgqp.cpp:708, batched over the node's GPUs. */
+int qpgpu_solve_batched_multi(const qpgpu_problem_desc* d, int32_t ndev, const int32_t* devices,
+                              double* G, const double* g0,
+                              const double* CE, const double* ce0,
+                              const double* CI, const double* ci0,
+                              double* x, double* f, int32_t* status, int32_t* iters);
+
 /* Convert one per-QP array of `elems` doubles per QP between the layouts on the device
  * (to_tiled = 1: QP-major -> TILED64, 0: back).  src and dst must not overlap; the TILED64
  * side holds ceil(batch/64) whole tiles (padding entries are left untouched / not read).

@@ -1244,60 +1244,67 @@ __global__ void __launch_bounds__(64, 1) QP_LANE_KERNEL(const QpArgs a) {
 #define QPGPU_LANE_PART 0
 #endif
 template <int NM, int MM, int T>
-static void launch_lane_p0(const QpArgs& a, hipStream_t stream);
+static hipError_t launch_lane_p0(const QpArgs& a, hipStream_t stream);
 template <int NM, int MM, int T>
-static void launch_lane_t(const QpArgs& a, hipStream_t stream) {
+static hipError_t launch_lane_t(const QpArgs& a, hipStream_t stream) {
   const int64_t blocks = (a.batch + kQpw - 1) / kQpw;
   const dim3 g((unsigned)blocks), blk(64);
+// A/B builds with one instantiation only refuse every other launch with an error: a launch
+// they skipped silently once returned the previous call's f / status / passes through the host
+// entry's reused device buffers, with x = 0 (profiles/r05_s26)
 #ifdef QPGPU_LANE_AB_C1ONLY
   // A/B experiment builds (tools/ab_build.sh): only the C1 instantiation, for a quick compile
   if constexpr (NM == 7 && MM == 14 && T == 1)
-    if (a.n == NM && a.m == MM && !a.x_eq && a.p == 6)
+    if (a.n == NM && a.m == MM && !a.x_eq && a.p == 6) {
       hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, 6>), g, blk, 0, stream, a);
-  return;
+      return hipSuccess;
+    }
+  return hipErrorInvalidValue;
 #endif
 #ifdef QPGPU_LANE_AB_N8P0ONLY
   // A/B / ISA-study builds: only the QP-major (8, 0, 16) instantiation
   if constexpr (NM == 8 && MM == 16 && T == 1)
-    if (a.n == NM && a.m == MM && !a.x_eq && a.p == 0)
+    if (a.n == NM && a.m == MM && !a.x_eq && a.p == 0) {
       hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, 0>), g, blk, 0, stream, a);
-  return;
+      return hipSuccess;
+    }
+  return hipErrorInvalidValue;
 #endif
   if (a.n == NM && a.m == MM && !a.x_eq) {
     if (a.p == 6)
       hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, 6>), g, blk, 0, stream, a);
     else if (a.p == 0)
-      launch_lane_p0<NM, MM, T>(a, stream);
+      return launch_lane_p0<NM, MM, T>(a, stream);
     else
       hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, -1>), g, blk, 0, stream, a);
   } else {
     hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, false, -1>), g, blk, 0, stream, a);
   }
+  return hipSuccess;
 }
 
 #if QPGPU_LANE_PART == 1
 }  // namespace QPK_LANE_NS
-extern "C" void qpk_launch_lane_p0(const qpk::QpArgs* a, hipStream_t stream);  // qp_lane_p0.hip
+extern "C" hipError_t qpk_launch_lane_p0(const qpk::QpArgs* a, hipStream_t stream);  // qp_lane_p0.hip
 namespace QPK_LANE_NS {
 template <int NM, int MM, int T>
-static void launch_lane_p0(const QpArgs& a, hipStream_t stream) {
-  qpk_launch_lane_p0(&a, stream);
+static hipError_t launch_lane_p0(const QpArgs& a, hipStream_t stream) {
+  return qpk_launch_lane_p0(&a, stream);
 }
 #else
 template <int NM, int MM, int T>
-static void launch_lane_p0(const QpArgs& a, hipStream_t stream) {
+static hipError_t launch_lane_p0(const QpArgs& a, hipStream_t stream) {
   const int64_t blocks = (a.batch + kQpw - 1) / kQpw;
   hipLaunchKernelGGL((QP_LANE_KERNEL<NM, MM, T, true, 0>), dim3((unsigned)blocks), dim3(64), 0, stream, a);
+  return hipSuccess;
 }
 #endif
 
 #if QPGPU_LANE_PART != 2
 template <int NM, int MM>
 static hipError_t launch_lane(const QpArgs& a, hipStream_t stream) {
-  if (a.tile == 64)
-    launch_lane_t<NM, MM, 64>(a, stream);
-  else
-    launch_lane_t<NM, MM, 1>(a, stream);
+  const hipError_t e = a.tile == 64 ? launch_lane_t<NM, MM, 64>(a, stream) : launch_lane_t<NM, MM, 1>(a, stream);
+  if (e != hipSuccess) return e;
   return hipGetLastError();
 }
 
@@ -1322,13 +1329,16 @@ const LaneVariant* pick_lane(int n, int m) {
 }  // namespace QPK_LANE_NS
 
 #if QPGPU_LANE_PART == 2
-// part 2: the exact p = 0 kernels only (the caller, part 1's launch_lane_t, has matched the shape)
-extern "C" void qpk_launch_lane_p0(const qpk::QpArgs* a, hipStream_t stream) {
+// part 2: the exact p = 0 kernels only (the caller, part 1's launch_lane_t, has matched the
+// shape).  A shape part 1 forwards that this list lacks (a LaneVariant added to kLaneVariants
+// without an entry here) is an error, never a silent success with nothing written.
+extern "C" hipError_t qpk_launch_lane_p0(const qpk::QpArgs* a, hipStream_t stream) {
   using namespace QPK_LANE_NS;
   if (a->n == 7 && a->m == 14)
-    a->tile == 64 ? launch_lane_p0<7, 14, 64>(*a, stream) : launch_lane_p0<7, 14, 1>(*a, stream);
-  else if (a->n == 8 && a->m == 16)
-    a->tile == 64 ? launch_lane_p0<8, 16, 64>(*a, stream) : launch_lane_p0<8, 16, 1>(*a, stream);
+    return a->tile == 64 ? launch_lane_p0<7, 14, 64>(*a, stream) : launch_lane_p0<7, 14, 1>(*a, stream);
+  if (a->n == 8 && a->m == 16)
+    return a->tile == 64 ? launch_lane_p0<8, 16, 64>(*a, stream) : launch_lane_p0<8, 16, 1>(*a, stream);
+  return hipErrorInvalidValue;
 }
 #else
 extern "C" hipError_t QPK_LANE_C(qpk_launch_lane)(const qpk::QpArgs* a, hipStream_t stream, int* handled,

@@ -7,10 +7,14 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/qpgpu.h"
 #include "qp_common.h"
@@ -281,8 +285,9 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
   auto launch_generic = [&]() -> int {
     if (!qpk_generic_covers(a.n, a.m)) return QPGPU_SUCCESS;  // handled stays 0
     const int64_t per = qpk_generic_workspace_bytes(a.n, a.m, 1);
+    if (per <= 0) return QPGPU_SUCCESS;  // handled stays 0
     int64_t chunk = a.batch;
-    if (per * a.batch > g_generic_ws_cap) {
+    if (a.batch > g_generic_ws_cap / per) {  // per * batch > cap, without the int64 overflow
       chunk = g_generic_ws_cap / per;
       if (a.tile == 64) chunk = chunk / 64 * 64;
       if (chunk < (a.tile == 64 ? 64 : 1)) chunk = a.tile == 64 ? 64 : 1;
@@ -443,7 +448,10 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const doubl
     put(oCI, CI, nCI);
     put(oci0, ci0, nci0);
     put(ox, x, nx);  // x passes through unchanged on NONPD
-    if ((e = hipMemcpyAsync(base, h, of, hipMemcpyHostToDevice, s)) != hipSuccess)
+    // f | status | iters poisoned (NaN, -1, -1) and sent with the inputs: outputs a kernel did
+    // not write never come back as the previous call's values from the reused device buffer
+    std::memset(h + of, 0xFF, total - of);
+    if ((e = hipMemcpyAsync(base, h, total, hipMemcpyHostToDevice, s)) != hipSuccess)
       return fail_drain(e, "hipMemcpyAsync H2D");
     rc = qpgpu_solve_batched(d, dG, D(og0), D(oCE), D(oce0), D(oCI), D(oci0), D(ox), D(of),
                              reinterpret_cast<int32_t*>(base + os),
@@ -473,6 +481,8 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const doubl
       (e = h2d(oCI, CI, nCI)) != hipSuccess || (e = h2d(oci0, ci0, nci0)) != hipSuccess ||
       (e = h2d(ox, x, nx)) != hipSuccess)  // x passes through unchanged on NONPD
     return fail_drain(e, "hipMemcpyAsync H2D");
+  // f | status | iters poisoned (NaN, -1, -1), as in the staged path
+  if ((e = hipMemsetAsync(base + of, 0xFF, total - of, s)) != hipSuccess) return fail_drain(e, "hipMemsetAsync");
   rc = qpgpu_solve_batched(d, dG, D(og0), D(oCE), D(oce0), D(oCI), D(oci0), D(ox), D(of),
                            reinterpret_cast<int32_t*>(base + os),
                            reinterpret_cast<int32_t*>(base + oi), s);
@@ -489,6 +499,118 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const doubl
     return fail_drain(e, "hipMemcpyAsync D2H");
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
   return QPGPU_SUCCESS;
+}
+
+// ---- several GPUs from one process (qpgpu_solve_batched_multi) ---------------------------------
+// One persistent worker thread per shard slot: slot k runs shard k's qpgpu_solve_batched_host on
+// the device the call names, with that thread's own device buffers, pinned staging and stream
+// (the host entry's thread_local state), so a slot's buffers are reused across calls and two
+// slots on the same device never share a stream.  Workers are detached and live for the process.
+namespace {
+struct ShardWorker {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::function<int()> job;
+  bool busy = false;
+  int rc = 0;
+  std::string err;
+  ShardWorker() {
+    std::thread([this] {
+      for (;;) {
+        std::function<int()> j;
+        {
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [this] { return job != nullptr; });
+          j = std::move(job);
+          job = nullptr;
+        }
+        const int r = j();
+        const std::string e = r == QPGPU_ERR_HIP ? g_last_error : std::string();
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          rc = r;
+          err = e;
+          busy = false;
+        }
+        cv.notify_all();
+      }
+    }).detach();
+  }
+  void submit(std::function<int()> j) {
+    std::lock_guard<std::mutex> lk(mu);
+    busy = true;
+    job = std::move(j);
+    cv.notify_all();
+  }
+  int wait(std::string* e) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [this] { return !busy; });
+    *e = err;
+    return rc;
+  }
+};
+std::mutex g_pool_mu;  // one multi-device call at a time owns the pool
+// never destroyed: a worker blocks on its condition variable until the process ends
+std::vector<ShardWorker*>& g_pool = *new std::vector<ShardWorker*>();
+}  // namespace
+
+int qpgpu_solve_batched_multi(const qpgpu_problem_desc* d, int32_t ndev, const int32_t* devices,
+                              double* G, const double* g0, const double* CE, const double* ce0,
+                              const double* CI, const double* ci0, double* x, double* f,
+                              int32_t* status, int32_t* iters) {
+  int rc = validate(d);
+  if (rc) return rc;
+  if (ndev <= 0 || ndev > 64 || !devices) return QPGPU_ERR_INVALID_ARGUMENT;
+  const int have = qpgpu_device_count();
+  if (have <= 0) {
+    g_last_error = "no HIP device visible";
+    return QPGPU_ERR_NO_DEVICE;
+  }
+  for (int k = 0; k < ndev; k++)
+    if (devices[k] < 0 || devices[k] >= have) return QPGPU_ERR_INVALID_ARGUMENT;
+  if (d->batch == 0) return QPGPU_SUCCESS;
+  if (!G || !g0 || !x || !f || !status) return QPGPU_ERR_INVALID_ARGUMENT;
+  if ((d->p > 0 && (!CE || !ce0)) || (d->m > 0 && (!CI || !ci0))) return QPGPU_ERR_INVALID_ARGUMENT;
+  if (!family_covers(d->flags, d->n, d->p, d->m)) return QPGPU_ERR_UNSUPPORTED_SHAPE;
+  const bool tiled = d->layout == QPGPU_LAYOUT_TILED64;
+  const int64_t B = d->batch, n = d->n, p = d->p, m = d->m;
+  // shard bounds: contiguous, whole tiles in TILED64 (a shard may come out empty)
+  std::vector<int64_t> lo(ndev + 1);
+  for (int k = 0; k <= ndev; k++) {
+    int64_t b = B * k / ndev;
+    if (tiled) b = (b + 63) / 64 * 64;
+    lo[k] = b < B ? b : B;
+  }
+  auto off = [&](int64_t b0, int64_t E) { return tiled ? (b0 / 64) * 64 * E : b0 * E; };
+  std::lock_guard<std::mutex> pool_hold(g_pool_mu);
+  while ((int)g_pool.size() < ndev) g_pool.emplace_back(new ShardWorker());
+  std::vector<int> used;
+  for (int k = 0; k < ndev; k++) {
+    const int64_t b0 = lo[k], cnt = lo[k + 1] - lo[k];
+    if (cnt <= 0) continue;
+    qpgpu_problem_desc dk = *d;
+    dk.batch = cnt;
+    const int dev = devices[k];
+    g_pool[k]->submit([=]() -> int {
+      hipError_t e = hipSetDevice(dev);
+      if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+      return qpgpu_solve_batched_host(&dk, G + off(b0, n * n), g0 + off(b0, n), CE ? CE + off(b0, n * p) : CE,
+                                      ce0 ? ce0 + off(b0, p) : ce0, CI ? CI + off(b0, n * m) : CI,
+                                      ci0 ? ci0 + off(b0, m) : ci0, x + off(b0, n), f + b0, status + b0,
+                                      iters ? iters + b0 : iters);
+    });
+    used.push_back(k);
+  }
+  int first = QPGPU_SUCCESS;
+  for (int k : used) {
+    std::string e;
+    const int r = g_pool[k]->wait(&e);
+    if (r && !first) {
+      first = r;
+      if (r == QPGPU_ERR_HIP) g_last_error = "device " + std::to_string(devices[k]) + ": " + e;
+    }
+  }
+  return first;
 }
 
 // Diagnostic hook (not in include/qpgpu.h): device buffer of kStampSlots uint64 per wave that

@@ -68,6 +68,7 @@ EXPORTED_SYMBOLS = (
     "qpgpu_device_count",
     "qpgpu_abi_version",
     "qpgpu_relayout",
+    "qpgpu_solve_batched_multi",
 )
 
 
@@ -100,6 +101,8 @@ def _load():
     lib.qpgpu_solve_batched_eq.restype = ctypes.c_int
     lib.qpgpu_solve_batched_host.argtypes = [ctypes.POINTER(ProblemDesc)] + [vp] * 10
     lib.qpgpu_solve_batched_host.restype = ctypes.c_int
+    lib.qpgpu_solve_batched_multi.argtypes = [ctypes.POINTER(ProblemDesc), ctypes.c_int32, vp] + [vp] * 10
+    lib.qpgpu_solve_batched_multi.restype = ctypes.c_int
     lib.qpgpu_kernel_name.argtypes = [ctypes.c_int32] * 3
     lib.qpgpu_kernel_name.restype = ctypes.c_char_p
     lib.qpgpu_kernel_name_flags.argtypes = [ctypes.c_int32] * 3 + [ctypes.c_uint32]
@@ -264,15 +267,25 @@ def algorithmic_bytes_per_qp(n: int, p: int, m: int) -> int:
 # ----------------------------------------------------------------------------------------------
 # host-pointer solve (numpy in, numpy out) — copies through the C-ABI's host entry point
 # ----------------------------------------------------------------------------------------------
+def _host_call(d, arrs, outs, devices):
+    """qpgpu_solve_batched_host, or qpgpu_solve_batched_multi over `devices` (device ids)."""
+    if devices is None:
+        return LIB.qpgpu_solve_batched_host(ctypes.byref(d), *[_ptr(a) for a in arrs], *[_ptr(o) for o in outs])
+    dv = np.ascontiguousarray(devices, dtype=np.int32)
+    return LIB.qpgpu_solve_batched_multi(ctypes.byref(d), len(dv), _ptr(dv), *[_ptr(a) for a in arrs],
+                                         *[_ptr(o) for o in outs])
+
+
 def solve_batched_host(pr: Problems, write_factor: bool = False, max_iter: int = 0, family=None,
-                       layout=None, exact: bool = False, fast: bool = False):
+                       layout=None, exact: bool = False, fast: bool = False, devices=None):
     """Solve every QP of `pr` on the GPU.  Returns (x, f, status, iters).
 
     With write_factor=True, pr.G is overwritten with each QP's Cholesky factor, as the
     reference overwrites G (QuadProg++.hh:42-45).  layout="tiled64" sends the batch in the
     TILED64 layout (converted here on the host) and converts x / G back.  exact=True keeps the
     reference's operation order for n > 64 as well (QPGPU_FLAG_EXACT); fast=True runs the lane
-    kernel's fast build (QPGPU_FLAG_FAST: within 1e-10, not bitwise)."""
+    kernel's fast build (QPGPU_FLAG_FAST: within 1e-10, not bitwise).  devices=[d0, d1, ...]
+    splits the batch into contiguous shards over those GPUs (qpgpu_solve_batched_multi)."""
     B, n, p, m = pr.batch, pr.n, pr.p, pr.m
     xflags = FAMILY_FLAGS[family] | (FLAG_EXACT if exact else 0) | (FLAG_FAST if fast else 0)
     if LAYOUTS[layout] == LAYOUT_TILED64:
@@ -283,8 +296,7 @@ def solve_batched_host(pr: Problems, write_factor: bool = False, max_iter: int =
         it = np.zeros(B, dtype=np.int32)
         d = ProblemDesc(n, p, m, max_iter, B,
                         (FLAG_WRITE_FACTOR if write_factor else 0) | xflags, LAYOUT_TILED64)
-        rc = LIB.qpgpu_solve_batched_host(ctypes.byref(d), *[_ptr(a) for a in arrs], _ptr(xt), _ptr(f),
-                                          _ptr(st), _ptr(it))
+        rc = _host_call(d, arrs, (xt, f, st, it), devices)
         _check(rc, "qpgpu_solve_batched_host")
         if write_factor:
             pr.G[...] = from_tiled64(arrs[0], B, (n, n))
@@ -299,8 +311,7 @@ def solve_batched_host(pr: Problems, write_factor: bool = False, max_iter: int =
     st = np.zeros(B, dtype=np.int32)
     it = np.zeros(B, dtype=np.int32)
     d = ProblemDesc(n, p, m, max_iter, B, (FLAG_WRITE_FACTOR if write_factor else 0) | xflags, 0)
-    rc = LIB.qpgpu_solve_batched_host(ctypes.byref(d), *[_ptr(a) for a in arrs], _ptr(x), _ptr(f),
-                                      _ptr(st), _ptr(it))
+    rc = _host_call(d, arrs, (x, f, st, it), devices)
     _check(rc, "qpgpu_solve_batched_host")
     return x, f, st, it
 

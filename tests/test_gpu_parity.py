@@ -384,14 +384,16 @@ def test_fast_other_lane_shapes(gpu, n, p, m):
     assert_fast_parity(qpgpu.make_problems("general", n, p, m, 0, 1001, seed=n * 100 + m), f"fast {(n, p, m)}")
 
 
+@pytest.mark.parametrize("layout", ["qp_major", "tiled64"])
 @pytest.mark.parametrize("name,pr", qp_cases.edge_cases(), ids=[c[0] for c in qp_cases.edge_cases()])
-def test_fast_edge_cases(gpu, name, pr):
+def test_fast_edge_cases(gpu, name, pr, layout):
     """Every exit of the algorithm through the fast build: same status; x, f within 1e-10 where the
     QP is solved.  Non-finite data (the -inf / NaN limits) makes the fast forms invalid on those
-    lanes, so their waves re-solve with IEEE divisions (lane_body<..., SAFE>)."""
+    lanes, so their waves re-solve with IEEE divisions (lane_body<..., SAFE>) — in both layouts,
+    since the re-solve body has its own TILED64 loads and stores."""
     if not covers("lane", pr.n, pr.m):
         pytest.skip("shape outside the lane kernel")
-    assert_fast_parity(pr, f"fast {name}")
+    assert_fast_parity(pr, f"fast {name}", layout=layout)
 
 
 def test_fast_flag_rules(gpu):
@@ -412,16 +414,31 @@ def test_fast_flag_rules(gpu):
     assert np.array_equal(xf.view(np.uint64), xd.view(np.uint64)) and np.array_equal(sf, sd)
 
 
-def test_fast_fallback_parity(gpu):
-    """Every wave of a full C1 batch holds one QP whose G is non-finite, so every wave's fast
+@pytest.mark.parametrize("layout", ["qp_major", "tiled64"])
+@pytest.mark.parametrize("kind,p", [("general", 6), ("box", 0)])
+def test_fast_fallback_parity(gpu, kind, p, layout):
+    """Every wave of a full C1 (C2) batch holds one QP whose G is non-finite, so every wave's fast
     attempt turns invalid in the setup and the wave re-solves with the IEEE forms: the results
-    still meet the fast contract.  (What the fallback costs in time is measured by
-    tools/fallback_cost.py, not asserted in the parity suite.)"""
+    still meet the fast contract, in both layouts (the re-solve body's TILED64 x store is its
+    own code).  (What the fallback costs in time is measured by tools/fallback_cost.py, not
+    asserted in the parity suite.)"""
     B = 65536
-    pr = qpgpu.make_problems("general", 7, 6, 14, 0, B, seed=31)
+    pr = qpgpu.make_problems(kind, 7, p, 14, 0, B, seed=31)
     bad = qpgpu.Problems(pr.n, pr.p, pr.m, pr.G.copy(), pr.g0, pr.CE, pr.ce0, pr.CI, pr.ci0)
     bad.G[5::64, 0, 0] = np.nan
-    assert_fast_parity(bad, "fast fallback (NaN G in every wave)")
+    assert_fast_parity(bad, f"fast fallback {kind} (NaN G in every wave)", layout=layout)
+
+
+def test_fast_loop_top_exit_regression(gpu):
+    """The round-4 wrong-result run (profiles/r04_s2/worst_base.log: qp_lane_fast<N=8,M=16> on
+    1 001 QPs of (8, 0, 16), seed 816, x off by up to 4e-2 on 4 QPs) with the
+    loop-top exit compiled in: every QP's data is finite and moderate, so no wave takes the
+    fallback, and x must stay within the fast contract (measured 4.7e-15 since round 5)."""
+    assert qpgpu.kernel_name(8, 0, 16, fast=True) == "qp_lane_fast<N=8,M=16>"
+    for layout in ("qp_major", "tiled64"):
+        ex, _ = assert_fast_parity(qpgpu.make_problems("general", 8, 0, 16, 0, 1001, seed=816),
+                                   f"loop-top regression {layout}", layout=layout)
+        assert ex <= 1e-12, ex
 
 
 # ---- QPGPU_FLAG_FAST for the wave kernel's LDS variants (n <= 64, m <= 256; DESIGN §5.7): the
@@ -462,8 +479,9 @@ def test_fast_wave_edge_cases(gpu, name, pr):
     assert_fast_parity(pr, f"fast wave {name}", family="wave")
 
 
+@pytest.mark.parametrize("layout", ["qp_major", "tiled64"])
 @pytest.mark.parametrize("n,p,m,B", [(30, 6, 60, 65), (32, 8, 64, 64), (24, 0, 60, 33), (14, 10, 28, 9)])
-def test_fast_wave_fallback_edges(gpu, n, p, m, B):
+def test_fast_wave_fallback_edges(gpu, n, p, m, B, layout):
     """Non-finite and extreme G entries in some QPs of a batch: those waves re-solve with the IEEE
     forms; status, passes and x, f of every QP as the oracle's (within 1e-10)."""
     pr = qp_cases.make("general", n, p, m, B, seed=n + B + 1)
@@ -472,7 +490,7 @@ def test_fast_wave_fallback_edges(gpu, n, p, m, B):
     pr.G[2, 2, 2] = np.inf
     pr.G[3, 4, 9] = 1.0e300
     pr.ci0[4, 1] = -np.inf
-    assert_fast_parity(pr, f"fast wave fallback n={n}")
+    assert_fast_parity(pr, f"fast wave fallback n={n} {layout}", layout=layout)
 
 
 # ---- the generic workspace kernel (qp_generic.hip): any n, p, m, bitwise with the reference's
@@ -552,3 +570,45 @@ def test_generic_sub_batches(gpu, layout, B):
                       write_factor=True, family="generic", layout=layout)
     finally:
         setcap(0)
+
+
+@pytest.mark.parametrize("layout,B", [("qp_major", 10), ("tiled64", 150)])
+def test_generic_sub_batches_eq(gpu, layout, B):
+    """The same sub-batches through qpgpu_solve_batched_eq: each sub-batch's x_eq /
+    f_eq / status_eq and iters are offset like x / f / status — the full solve and the m = 0
+    snapshot bitwise against the oracle across every sub-batch boundary."""
+    import ctypes
+
+    import torch
+
+    n, p, m = 40, 5, 90
+    qpgpu.LIB.qpk_generic_workspace_bytes.restype = ctypes.c_int64
+    qpgpu.LIB.qpk_generic_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64]
+    per = qpgpu.LIB.qpk_generic_workspace_bytes(n, m, 1)
+    setcap = qpgpu.LIB.qpgpu_debug_set_generic_ws_cap
+    setcap.argtypes = [ctypes.c_int64]
+    pr = qp_cases.make("general", n, p, m, B, seed=B + 1)
+    db = qpgpu.DeviceBatch(pr, "cuda:0", with_iters=True, layout=layout)
+    xe = torch.full_like(db.x, float("nan"))
+    fe = torch.full_like(db.f, float("nan"))
+    se = torch.full_like(db.status, -7)
+    setcap(3 * per)
+    try:
+        db.solve(family="generic", eq_out=(xe, fe, se))
+        torch.cuda.synchronize()
+    finally:
+        setcap(0)
+    x, f, st, it = db.results()
+    xo, fo, so, io = oracle.solve_batch(qpgpu.Problems(n, p, m, pr.G.copy(), pr.g0, pr.CE, pr.ce0, pr.CI, pr.ci0),
+                                        max_steps=1000 + 100 * (n + p + m))
+    assert np.array_equal(so, st) and np.array_equal(io, it)
+    assert np.array_equal(fo.view(np.uint64), f.view(np.uint64))
+    assert np.array_equal(xo.view(np.uint64), x.view(np.uint64))
+    pr0 = qpgpu.Problems(n, p, 0, pr.G.copy(), pr.g0, pr.CE, pr.ce0, np.zeros((B, n, 0)), np.zeros((B, 0)))
+    x0, f0, s0, _ = oracle.solve_batch(pr0)
+    xe = xe.cpu().numpy()
+    if layout == "tiled64":
+        xe = qpgpu.from_tiled64(xe.reshape(-1), B, (n,))
+    assert np.array_equal(se.cpu().numpy(), s0)
+    assert np.array_equal(fe.cpu().numpy().view(np.uint64), f0.view(np.uint64))
+    assert np.array_equal(xe.view(np.uint64), x0.view(np.uint64))
