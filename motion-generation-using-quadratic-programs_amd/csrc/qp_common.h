@@ -345,6 +345,30 @@ constexpr uint32_t kArgAligned16 = 0x80000000u;
 // internal QpArgs.flags bit: the workspace already holds the setup (qp_panel.hip) — J, x0, f0,
 // c1, c2 and the Cholesky status — so the loop kernel starts at the equality phase
 constexpr uint32_t kSetupDone = 0x40000000u;
+// internal QpArgs.flags bit: the EXACT re-solve launch after a tolerance-mode launch — only the
+// QPs whose status carries kStResolve are solved (one QP per workgroup: the others exit at once)
+constexpr uint32_t kResolveOnly = 0x20000000u;
+// Tolerance mode (n > 64 default: MFMA panel setup + tree sums) certification.  A QP one of whose
+// decisions the tolerance arithmetic cannot certify against the reference's rounding is marked in
+// its status word (kStResolve | reason << kStReasonShift) and re-solved by the EXACT launch, which
+// writes the plain status back.  Reasons:
+enum : int {
+  kUncDependent = 1 << 0,   // add_constraint: |d_iq| <= 1e6 eps R_norm (rank-deficient / near-dependent column)
+  kUncSetup = 1 << 1,       // panel setup: not positive definite, or pivots spread beyond 1e8
+  kUncMaxIter = 1 << 2,     // the step cap fired
+  kUncStepTie = 1 << 3,     // t1 and t2 within 1e-9 relative (partial vs full step)
+  kUncZz = 1 << 4,          // z.z within [eps/4, 4 eps] of the reference's |z.z| > eps test
+  kUncTt2 = 1 << 5,         // |t - t2| within [eps/4, 4 eps] of the full-step test
+  kUncSelTie = 1 << 6,      // two most violated constraints within 1e-9 relative
+  kUncPsi = 1 << 7,         // |psi| within [thr/4, 4 thr] of the stop test
+  kUncFCancel = 1 << 8,     // the objective cancels: max |f| over the run > 1e4 |f|
+  kUncXCancel = 1 << 9,     // x cancels: max ||x||_inf over the run > 1e4 ||x||_inf
+  kUncNonFinite = 1 << 10,  // a non-finite x or f (infeasible included)
+  kUncT1Tie = 1 << 11,      // two blocking constraints' u/r within 1e-9 relative
+  kUncGivens = 1 << 12      // a Givens length within [eps/4, 4 eps] of the |h| < eps skip
+};
+constexpr int kStResolve = 0x100;
+constexpr int kStReasonShift = 9;
 
 // Per-QP device workspace of the large-QP path (n > 64, qp_wave.hip GJR + qp_panel.hip):
 //   [0, OFF_R)        J, COLUMN-major: J[k][j] at j*JS + k

@@ -64,6 +64,8 @@ __global__ void __launch_bounds__(256) qp_panel_setup_kernel(const QpArgs a, dou
     double c1 = 0.0;
     for (int i = 0; i < n; i++) c1 += Gb[(int64_t)(i * n + i) * T];
     shd[0] = c1;
+    shd[2] = __builtin_inf();  // smallest / largest pivot (certification of the loop, H[4])
+    shd[3] = 0.0;
     shi[0] = 0;
   }
   __syncthreads();
@@ -88,6 +90,10 @@ __global__ void __launch_bounds__(256) qp_panel_setup_kernel(const QpArgs a, dou
           break;
         }
         const double dg = sqrt(piv);
+        if (lane == 0 && k * 16 + c < n) {  // (the padding's identity pivots excluded)
+          shd[2] = fmin(shd[2], piv);
+          shd[3] = fmax(shd[3], piv);
+        }
         sg_sync();
         if (lane < 16) {
           if (lane > c)
@@ -244,6 +250,7 @@ __global__ void __launch_bounds__(256) qp_panel_setup_kernel(const QpArgs a, dou
     H[1] = 0.5 * f;
     H[2] = shd[0];
     H[3] = c2;
+    H[4] = shd[3] / shd[2];  // pivot spread: the loop marks QPs beyond 1e8 for the EXACT re-solve
   }
 }
 

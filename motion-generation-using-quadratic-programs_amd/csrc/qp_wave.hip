@@ -208,6 +208,59 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return ((r[0] + r[1]) + r[2]) + r[3];
 }
 
+// Sixteen sums over the wave's 64 lanes at once (tolerance mode's d = J^T np, 16 columns per
+// chunk): a reduce-scatter instead of sixteen full butterflies — v_permlane32_swap (lanes l, l^32),
+// v_permlane16_swap (l, l^16 within each half), DPP row_mirror (i, 15-i) and row_half_mirror
+// (i, 7-i) each halve the columns a lane carries while doubling the lanes summed, then two quad
+// butterflies finish; ~60 instructions instead of ~370.  Lane l ends with the full sum of column
+// colsum16_col(l) (the four lanes of a quad hold the same value, a + b == b + a).
+__device__ __forceinline__ void swap_pl32(double& a, double& b) {
+  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+  const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)ua, (uint32_t)ub, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(ua >> 32), (uint32_t)(ub >> 32), false, false);
+  a = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | (uint32_t)lo[0]);
+  b = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | (uint32_t)lo[1]);
+}
+__device__ __forceinline__ void swap_pl16(double& a, double& b) {
+  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+  const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)ua, (uint32_t)ub, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(ua >> 32), (uint32_t)(ub >> 32), false, false);
+  a = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | (uint32_t)lo[0]);
+  b = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | (uint32_t)lo[1]);
+}
+__device__ __forceinline__ int colsum16_col(int lane) {
+  return ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane & 15) >= 8) * 2 + ((lane & 7) >= 4);
+}
+__device__ __forceinline__ double colsum16(double (&v)[16]) {
+  const int l = threadIdx.x & 63;
+  double w[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) {  // lanes < 32 keep columns 0..7, lanes >= 32 columns 8..15
+    double a = v[u], b = v[u + 8];
+    swap_pl32(a, b);
+    w[u] = a + b;
+  }
+  double x[4];
+#pragma unroll
+  for (int u = 0; u < 4; u++) {  // within each half: lanes 0..15 keep slots 0..3, 16..31 slots 4..7
+    double a = w[u], b = w[u + 4];
+    swap_pl16(a, b);
+    x[u] = a + b;
+  }
+  const bool lo8 = (l & 15) < 8, lo4 = (l & 7) < 4;
+  double y[2];
+#pragma unroll
+  for (int u = 0; u < 2; u++) {  // row_mirror pairs i with 15 - i: i < 8 keeps slots 0..1
+    const double keep = lo8 ? x[u] : x[u + 2], send = lo8 ? x[u + 2] : x[u];
+    y[u] = keep + dpp_f64<0x140>(send);
+  }
+  // row_half_mirror pairs i with 7 - i: (i & 7) < 4 keeps slot 0
+  double z = (lo4 ? y[0] : y[1]) + dpp_f64<0x141>(lo4 ? y[1] : y[0]);
+  z += dpp_f64<0xB1>(z);  // quad xor 1
+  z += dpp_f64<0x4E>(z);  // quad xor 2
+  return z;
+}
+
 // Register-resident setup for the one-wave variants (S <= 64, LDS J/R, launched at one wave per
 // SIMD so registers are plentiful): lane j keeps row j of G/L (Cholesky), lane r builds row r of
 // J = L^{-T} by column-oriented forward substitution, and cholesky_solve runs across the lanes
@@ -277,8 +330,15 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 // per-QP control block (lead lane writes, subgroup reads after grp_sync)
 struct Ctl {
   double f, t, t1, t2, ss, R_norm, c1, c2, psi, ci0ip, znp;
+  // tolerance-mode certification (qp_common.h kUnc*): max |f| over the run, and the bits of
+  // ||x||_inf at the end / of max ||x||_inf over the run (non-negative doubles order as integers)
+  double fmax;
+  unsigned long long xn, xh;
+  // tolerance mode: bits of max_i ||CI[:, i]||_1 and max_i |ci0_i| (the scale of an s_i's rounding)
+  unsigned long long cim, c0m;
   int iq, ip, l, status, phase, iter, steps, flags, qq, ngiv, fin;
-  int pad[5];
+  int unc;  // tolerance mode: kUnc* reasons this QP's decisions are not certified
+  int pad[4];
 };
 
 enum : int {
@@ -451,6 +511,21 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
 #define L_(i, j) Lm[(i) * JS + (j)]
   // setup already in the workspace (qp_panel.hip): start from its header
   const bool pre = GJR && (a.flags & kSetupDone);
+  // certification (tolerance mode only): max |x_i| over the run into ctl->xh (kUncXCancel), an
+  // LDS atomic per update (a register for it spilled the 128-VGPR workspace kernel)
+  // certification: the scale of one s_i's rounding, max ||CI_i||_1 max ||x||_inf + max |ci0_i|
+  [[maybe_unused]] auto sigma_s = [&]() -> double {
+    const double cim = __builtin_bit_cast(double, (uint64_t)ctl->cim);
+    const double c0m = __builtin_bit_cast(double, (uint64_t)ctl->c0m);
+    const double xh = __builtin_bit_cast(double, (uint64_t)ctl->xh);
+    return cim * xh + c0m;
+  };
+  auto note_x = [&](double v) {
+    if (pre) {
+      const double av = fabs(v);
+      atomicMax(&ctl->xh, (unsigned long long)__builtin_bit_cast(uint64_t, av < dinf() ? av : 0.0));
+    }
+  };
 
   // ------------------------------------------------------------------ setup
   qp_stamp(a, 0);
@@ -465,12 +540,18 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
       ctl->c1 = H[2];
       ctl->c2 = H[3];
       ctl->R_norm = 1.0;
+      // certification: a failed or badly spread panel factorization (H[4] = max / min pivot)
+      ctl->unc = (ctl->status != QPGPU_QP_OK || !(H[4] <= 1e4)) ? kUncSetup : 0;
+      ctl->fmax = fabs(H[1]);
+      ctl->xn = ctl->xh = ctl->cim = ctl->c0m = 0ull;
       ctl->iq = 0;
       ctl->phase = live ? PH_SCAN : PH_DONE;
     }
     if (live)
       for (int i = ls; i < n; i += S) xv[i] = H[BigWs<NMAX>::HX + i];
     grp_sync<S>();
+    if (live)
+      for (int i = ls; i < n; i += S) note_x(xv[i]);  // (ctl->xh was cleared before the sync)
   }
   // G -> R region (becomes L), g0 -> z region
   if (live && !pre) {
@@ -493,6 +574,7 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
     for (int i = ls; i < n; i += S) zv[i] = EL(g0b, i);
   }
   if (lead && !pre) {
+    ctl->unc = 0;
     ctl->status = QPGPU_QP_OK;
     ctl->iter = 0;
     ctl->steps = 0;
@@ -781,14 +863,16 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
           double z = 0.0;
           int buf = 0;
           // d (and z) for the kDC values v of this lane's row; col(u) = their column or -1
+          static_assert(kDC == 16, "colsum16 reduces 16 columns per chunk");
+          const int c16 = colsum16_col(ls & 63);
           auto chunk = [&](const double* v, auto col) {
             double* const P = T + buf * (4 * kDC);
             buf ^= 1;
+            double pv[kDC];
 #pragma unroll
-            for (int u = 0; u < kDC; u++) {
-              const double w = wave_sum_f64(v[u] * npr);
-              if ((ls & 63) == 0) P[wv * kDC + u] = w;
-            }
+            for (int u = 0; u < kDC; u++) pv[u] = v[u] * npr;
+            const double w = colsum16(pv);
+            if ((ls & 3) == 0) P[wv * kDC + c16] = w;
             __syncthreads();
 #pragma unroll
             for (int u = 0; u < kDC; u++) {
@@ -1407,6 +1491,7 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
         iq++;
         ctl->iq = iq;
         const double dd = fabs(dv[iq - 1]);
+        if (pre && dd <= 1e6 * kEps * ctl->R_norm) ctl->unc |= kUncDependent;
         if (dd <= kEps * ctl->R_norm) {
           ctl->fin = 0;
         } else {
@@ -1484,6 +1569,7 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
         for (int j = qq; j < iq; j++) {
           double cc = R_(j, j), ss = R_(j + 1, j);
           const double h = wdist<F>(cc, ss, fok);
+          if (pre && fabs(h) >= 0.25 * kEps && fabs(h) <= 4.0 * kEps) ctl->unc |= kUncGivens;
           if (fabs(h) < kEps) {
             GF_(ng++) = 0.0;
             continue;
@@ -1592,12 +1678,19 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
         ctl->t2 = t2;
         uv[iq] = t2;
         ctl->f += 0.5 * (t2 * t2) * znp;
+        if (pre) {
+          if (fabs(zz) >= 0.25 * kEps && fabs(zz) <= 4.0 * kEps) ctl->unc |= kUncZz;
+          ctl->fmax = fmax(ctl->fmax, fabs(ctl->f));
+        }
         Av[i] = -i - 1;
       }
       grp_sync<S>();
       {
         const double t2 = ctl->t2;
-        for (int k = ls; k < n; k += S) xv[k] += t2 * zv[k];
+        for (int k = ls; k < n; k += S) {
+          xv[k] += t2 * zv[k];
+          note_x(xv[k]);
+        }
       }
       const uint64_t e3 = clk();
       teq[2] += e3 - e2;
@@ -1630,6 +1723,17 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
 
   qp_stamp(a, 3);
   if (any_bad()) return false;  // the fast attempt's setup / equality phase went out of range
+  if (GJR && pre && live) {
+    // certification: the scales of the s_i's rounding (sigma_s), one extra read of CI per QP
+    for (int i = ls; i < m; i += S) {
+      double a1 = 0.0;
+      for (int j = 0; j < n; j++) a1 += fabs(EL(CIb, j * m + i));
+      const double c0 = fabs(EL(ci0b, i));
+      atomicMax(&ctl->cim, (unsigned long long)__builtin_bit_cast(uint64_t, a1));
+      atomicMax(&ctl->c0m, (unsigned long long)__builtin_bit_cast(uint64_t, c0));
+    }
+    grp_sync<S>();
+  }
   // ------------------------------------------------------------------ active-set loop
   // Per-subgroup state machine; a wave loops until all of its QPs are done.
   const int max_steps = a.max_steps;
@@ -1752,19 +1856,29 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
       grp_sync<S>();
       if (lead) {
         double psi = 0.0;
+        int negc = 0;  // (certification: the negative s_i psi sums)
         constexpr int U = 8;  // loads of a chunk together, adds in i order
         auto chunk = [&](int ib, int c) {
           double sc[U];
 #pragma unroll
           for (int u = 0; u < U; u++) sc[u] = sv[ib + u];  // past m: in-bounds LDS, masked
 #pragma unroll
-          for (int u = 0; u < U; u++) psi += (u < c && sc[u] < 0.0) ? sc[u] : 0.0;
+          for (int u = 0; u < U; u++) {
+            psi += (u < c && sc[u] < 0.0) ? sc[u] : 0.0;
+            negc += (u < c && sc[u] < 0.0) ? 1 : 0;
+          }
         };
         int ib = 0;
         for (; ib + U <= m; ib += U) chunk(ib, U);
         if (ib < m) chunk(ib, m - ib);
         ctl->ss = 0.0;
         ctl->ip = 0;
+        if (pre) {
+          // the stop test |psi| <= thr within the rounding the two evaluations of the negative
+          // s_i can differ by: each s_i by at most 1e-10 (||CI_i||_1 ||x||_inf + |ci0_i|)
+          const double thr = (double)m * kEps * ctl->c1 * ctl->c2 * 100.0;
+          if (fabs(fabs(psi) - thr) <= 1e-4 * thr + 1e-10 * sigma_s() * negc) ctl->unc |= kUncPsi;
+        }
         if (fabs(psi) <= (double)m * kEps * ctl->c1 * ctl->c2 * 100.0) {
           ctl->phase = PH_DONE;
         } else {
@@ -1800,6 +1914,55 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
           sg_argmin<S>(sbest, ibest);
         }
       }
+      // workspace variant (one QP per 256-thread block): the same selection across the block —
+      // each lane scans its constraints in index order, then a butterfly per wave and the four
+      // waves' results in wave order; (value, index) pairs merge by value then lower index, so
+      // the result is the reference's (smallest s below the carried ss, first index) bit for bit,
+      // with the runner-up value for the certification (kUncSelTie)
+      [[maybe_unused]] double s2best = inf;
+      if constexpr (GJR && !kLaneSel) {
+        const double ss0 = ctl->ss;
+        for (int i = ls; i < m; i += S) {
+          const double v = sv[i];
+          if (v < ss0 && !act[i] && !exc[i]) {
+            if (v < sbest) {
+              s2best = sbest;
+              sbest = v;
+              ibest = i;
+            } else if (v < s2best) {
+              s2best = v;
+            }
+          }
+        }
+        auto merge = [&](double c1, int j1, double c2) {
+          if (c1 < sbest || (c1 == sbest && j1 < ibest)) {
+            s2best = fmin(sbest, c2);
+            sbest = c1;
+            ibest = j1;
+          } else {
+            s2best = fmin(s2best, c1);
+          }
+        };
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+          const double c1 = __shfl_xor(sbest, o, 64), c2 = __shfl_xor(s2best, o, 64);
+          const int j1 = __shfl_xor(ibest, o, 64);
+          merge(c1, j1, c2);
+        }
+        double* const W = Q + Ly.off_tsc;  // (the d/z pass's partials are not live here)
+        if ((ls & 63) == 0) {
+          W[3 * (ls >> 6)] = sbest;
+          W[3 * (ls >> 6) + 1] = (double)ibest;
+          W[3 * (ls >> 6) + 2] = s2best;
+        }
+        grp_sync<S>();
+        if (lead) {
+          sbest = W[0];
+          ibest = (int)W[1];
+          s2best = W[2];
+          for (int w = 1; w < S / 64; w++) merge(W[3 * w], (int)W[3 * w + 1], W[3 * w + 2]);
+        }
+      }
       if (lead) {
         double ss = ctl->ss;
         int ip = ctl->ip;
@@ -1807,6 +1970,15 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
           if (ibest != INT_MAX) {
             ss = sbest;
             ip = ibest;
+          }
+        } else if (GJR) {
+          if (ibest != INT_MAX) {
+            ss = sbest;
+            ip = ibest;
+            // two candidates within the rounding the two evaluations of s can differ by: a
+            // decision the tolerance mode's rounding may order differently (kUncSelTie)
+            if (pre && s2best < inf && s2best - sbest <= 2e-10 * sigma_s() + 1e-12 * (fabs(sbest) + fabs(s2best)))
+              ctl->unc |= kUncSelTie;
           }
         } else {
           for (int i = 0; i < m; i++)
@@ -1886,6 +2058,20 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
           t1 = t1best;
           l = Av[kbest];
         }
+      } else if (pre) {
+        double t1b = inf;  // runner-up (kUncT1Tie)
+        for (int k = p; k < iq; k++)
+          if (rv[k] > 0.0) {
+            const double q = uv[k] / rv[k];
+            if (q < t1) {
+              t1b = t1;
+              t1 = q;
+              l = Av[k];
+            } else if (q < t1b) {
+              t1b = q;
+            }
+          }
+        if (t1b < inf && t1b - t1 <= 1e-9 * (fabs(t1) + fabs(t1b))) ctl->unc |= kUncT1Tie;
       } else {
         for (int k = p; k < iq; k++)
           if (rv[k] > 0.0 && uv[k] / rv[k] < t1) {
@@ -1906,6 +2092,11 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
       ctl->t1 = t1;
       ctl->t2 = t2;
       ctl->l = l;
+      if (pre) {
+        if (fabs(zz) >= 0.25 * kEps && fabs(zz) <= 4.0 * kEps) ctl->unc |= kUncZz;
+        if (t1 < inf && t2 < inf && fabs(t1 - t2) <= 1e-9 * fmax(fabs(t1), fabs(t2))) ctl->unc |= kUncStepTie;
+        if (fabs(t - t2) >= 0.25 * kEps && fabs(t - t2) <= 4.0 * kEps) ctl->unc |= kUncTt2;
+      }
       if (t >= inf) {
         ctl->status = QPGPU_QP_INFEASIBLE;
         ctl->f = inf;
@@ -1917,6 +2108,7 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
         kind = 2;
       } else {
         ctl->f += t * znp * (0.5 * t + uv[iq]);
+        if (pre) ctl->fmax = fmax(ctl->fmax, fabs(ctl->f));
         uv[iq] += t;
         kind = (fabs(t - t2) < kEps) ? 3 : 4;
       }
@@ -1941,7 +2133,10 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
     }
     {
       const double t = ctl->t;
-      for (int k = ls; k < n; k += S) xv[k] += t * zv[k];
+      for (int k = ls; k < n; k += S) {
+        xv[k] += t * zv[k];
+        note_x(xv[k]);
+      }
     }
     grp_sync<S>();
     if (kind == 3) {
@@ -2005,6 +2200,28 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
   }
   // ------------------------------------------------------------------ outputs
   if (any_bad()) return false;
+  if (GJR && pre && live) {
+    // certification at the end: x's norm against its largest value over the run (cancellation),
+    // non-finite results, the step cap; a QP with any reason is marked for the EXACT re-solve
+    if (ls < n) {
+      const double xi = fabs(xv[ls]);
+      if (!(xi < inf)) atomicOr(&ctl->unc, kUncNonFinite);
+      atomicMax(&ctl->xn, (unsigned long long)__builtin_bit_cast(uint64_t, xi < inf ? xi : 0.0));
+    }
+    grp_sync<S>();
+    if (lead) {
+      const double xn = __builtin_bit_cast(double, (uint64_t)ctl->xn);
+      const double xh = __builtin_bit_cast(double, (uint64_t)ctl->xh);
+      const double fv = ctl->f;
+      int u = ctl->unc;
+      if (ctl->status == QPGPU_QP_MAX_ITER) u |= kUncMaxIter;
+      if (!(fabs(fv) < inf)) u |= kUncNonFinite;
+      if (!(ctl->fmax <= 1e4 * fabs(fv))) u |= kUncFCancel;
+      if (!(xh <= 1e4 * xn)) u |= kUncXCancel;
+      ctl->unc = u;
+    }
+    grp_sync<S>();
+  }
   if (live) {
     const int st = ctl->status;
     if (st != QPGPU_QP_NOT_POSITIVE_DEFINITE) {
@@ -2013,7 +2230,8 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
     }
     if (lead) {
       a.f[b] = ctl->f;
-      a.status[b] = st;
+      const int unc = (GJR && pre) ? ctl->unc : 0;
+      a.status[b] = unc ? (st | kStResolve | (unc << kStReasonShift)) : st;
       if (a.iters) a.iters[b] = ctl->iter;
     }
   }
@@ -2024,6 +2242,14 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
 template <int S, int NMAX, int MMAX, bool GJR, int OCC = 1>
 __global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
     QP_WAVE_KERNEL(const QpArgs a, double* __restrict__ ws) {
+  if constexpr (GJR) {
+    // the EXACT re-solve after a tolerance-mode launch: only the QPs marked for it (one QP per
+    // workgroup, so the exit is uniform)
+    if (a.flags & kResolveOnly) {
+      const int64_t b = blockIdx.x;
+      if (b >= a.batch || !(a.status[b] & kStResolve)) return;
+    }
+  }
   if constexpr (kWaveFast && !GJR && S <= 64) {
     if (!wave_body<S, NMAX, MMAX, GJR, OCC, true>(a, ws)) {
       __syncthreads();  // the fast attempt's LDS traffic is over
@@ -2163,6 +2389,7 @@ extern "C" hipError_t qpk_launch_panel_setup(const qpk::QpArgs* a, hipStream_t s
 // (QPGPU_FLAG_WRITE_FACTOR: the reference's bits), which the serial restatement here provides.
 // Only panel-set-up launches run the tolerance-mode loop, whose deferred J sweep may still be
 // pending when a QP finishes (see `pend` in qp_wave_kernel): keep both flags out of it.
+static bool g_resolve = true;
 static bool uses_panel(const qpk::WaveVariant* v, uint32_t flags) {
   return v->ws_doubles_per_qp > 0 && !(flags & (QPGPU_FLAG_EXACT | QPGPU_FLAG_WRITE_FACTOR));
 }
@@ -2181,8 +2408,17 @@ extern "C" hipError_t qpk_launch_medium_ws(const qpk::QpArgs* a, hipStream_t str
     if (e != hipSuccess) return e;
     qpk::QpArgs b = *a;
     b.flags |= qpk::kSetupDone;
-    return v->launch(b, stream, ws);
+    e = v->launch(b, stream, ws);
+    if (e != hipSuccess || !g_resolve) return e;
+    // the QPs the tolerance mode could not certify (status | kStResolve) again in the reference's
+    // operation order: one more launch whose other workgroups exit at once
+    qpk::QpArgs c = *a;
+    c.flags |= QPGPU_FLAG_EXACT | qpk::kResolveOnly;
+    return v->launch(c, stream, ws);
   }
   return v->launch(*a, stream, ws);
 }
+// test / diagnostic hook (qpgpu_debug_set_resolve): 0 leaves the tolerance mode's marks in
+// the status words and skips the EXACT re-solve
+extern "C" void qpk_set_resolve(int on) { g_resolve = on != 0; }
 #endif  // QPGPU_WAVE_FAST

@@ -617,6 +617,11 @@ int qpgpu_solve_batched_multi(const qpgpu_problem_desc* d, int32_t ndev, const i
 // the next launches fill with s_memtime phase stamps; NULL turns it off.
 void qpgpu_debug_set_stamps(void* dev_buf) { g_stamps = static_cast<uint64_t*>(dev_buf); }
 
+// Test hook (not in include/qpgpu.h): 0 skips the n > 64 default path's EXACT re-solve of the
+// QPs its tolerance mode did not certify, leaving their marks (0x100 | reasons << 9) in status.
+extern "C" void qpk_set_resolve(int on);
+void qpgpu_debug_set_resolve(int on) { qpk_set_resolve(on); }
+
 // Test hook (not in include/qpgpu.h): the generic kernel's per-launch workspace cap in bytes
 // (<= 0 restores the 4 GiB default), so the sub-batch path runs on small shapes.
 void qpgpu_debug_set_generic_ws_cap(int64_t bytes) { g_generic_ws_cap = bytes > 0 ? bytes : ((int64_t)4 << 30); }

@@ -154,6 +154,33 @@ def kernel_name(n: int, p: int, m: int, fast: bool = False) -> str:
     return LIB.qpgpu_kernel_name(n, p, m).decode()
 
 
+# the n > 64 default path's certification: a QP whose decisions the tolerance mode
+# cannot certify carries STATUS_RESOLVE | reasons << 9 until the EXACT re-solve rewrites it
+STATUS_RESOLVE = 0x100
+UNC_REASONS = ("dependent", "setup", "max_iter", "step_tie", "zz", "t_t2", "select_tie", "psi",
+               "f_cancel", "x_cancel", "non_finite", "t1_tie", "givens")
+
+
+def set_resolve(on: bool) -> None:
+    """Test / diagnostic hook: False skips the EXACT re-solve of uncertified n > 64 QPs and leaves
+    their marks in the status words (see unc_reasons)."""
+    fn = LIB.qpgpu_debug_set_resolve
+    fn.argtypes = [ctypes.c_int]
+    fn(1 if on else 0)
+
+
+def unc_reasons(status: np.ndarray) -> dict:
+    """Counts of each certification reason in status words returned with set_resolve(False)."""
+    st = np.asarray(status, dtype=np.int64)
+    marked = (st & STATUS_RESOLVE) != 0
+    out = {"marked": int(marked.sum())}
+    for k, name in enumerate(UNC_REASONS):
+        c = int((marked & (((st >> 9) >> k) & 1).astype(bool)).sum())
+        if c:
+            out[name] = c
+    return out
+
+
 def device_count() -> int:
     return int(LIB.qpgpu_device_count())
 
