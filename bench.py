@@ -120,10 +120,11 @@ def parse(argv=None):
     ap.add_argument("--input-sets", type=int, default=0,
                     help="distinct resident input sets the steps rotate over (0 = enough to "
                          "defeat the Infinity Cache, 1 = warm)")
-    ap.add_argument("--kernel-reps", type=int, default=20,
-                    help="serialized launches timed for the roofline's kernel duration")
-    ap.add_argument("--kernel-rounds", type=int, default=5,
-                    help="rounds of --kernel-reps launches (median round reported)")
+    ap.add_argument("--kernel-reps", type=int, default=None,
+                    help="serialized launches timed for the roofline's kernel duration (default 20; "
+                         "C5: 3, whose launch takes ~0.24 s)")
+    ap.add_argument("--kernel-rounds", type=int, default=None,
+                    help="rounds of --kernel-reps launches (median round reported; default 5, C5: 3)")
     ap.add_argument("--prewarm-ms", type=float, default=40.0,
                     help="untimed solver steps for this long before the warmup steps (GPU clocks)")
     ap.add_argument("--kernel-warmup", type=int, default=-1,
@@ -163,6 +164,12 @@ def spawn_ranks(args):
            f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
            f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
     return subprocess.call(cmd, env=dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4")))
+
+
+def progress(msg):
+    """A phase marker on stderr (the JSON line stays the only stdout line): long configurations
+    (C5: ~0.24 s per launch, a 4 096-QP oracle parity pass) keep reporting while they run."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def cpu_chunk(pr):
@@ -280,6 +287,7 @@ def cpu_baseline(pr, seconds, layout, gpu_out=None):
     if gpu_out is not None:
         P = parity_qps(pr)
         t0 = time.perf_counter()
+        progress(f"parity: the oracle re-solves {P} QPs on {threads} threads")
         xo, fo, so, _ = oracle.solve_batch(pr.slice(0, P), max_steps=cap, threads=threads)
         rec = parity_record(pr, layout, gpu_out, (xo, fo, so),
                             f"oracle/qp_oracle.c on the same QPs ({threads} threads, "
@@ -341,6 +349,10 @@ def main():
 
     cfg = args.config or ("C1" if world == 1 else "C4")
     kind, n, p, m, bdef, desc = CONFIGS[cfg]
+    if args.kernel_reps is None:
+        args.kernel_reps = 3 if cfg == "C5" else 20
+    if args.kernel_rounds is None:
+        args.kernel_rounds = 3 if cfg == "C5" else 5
     if args.warmup is None:
         args.warmup = DEFAULT_STEPS[cfg][0]
     if args.steps is None:
@@ -451,6 +463,7 @@ def main():
     sync_all()
     prewarm = {"steps": k_pw, "ms": round((time.perf_counter() - t_pw) * 1e3, 2),
                "note": "untimed solver steps before the W warmup steps (steady-state clocks)"}
+    progress(f"{cfg}: timed region, {args.steps} steps after {args.warmup} warmup")
     elapsed = timed(args.steps, args.warmup, S, args.gather if gat else "none")
     # the last step of every stream slot, checked against set 0's solve rotated (guards the
     # pipelining and the rotated sets): x, f, status bit for bit
@@ -540,7 +553,9 @@ def main():
             kernel_rounds[key] = rounds
         return float(np.median(rounds))
 
+    progress(f"{cfg}: kernel-duration rounds")
     kern_cold = kernel_ms(True, key="cold")
+    progress(f"{cfg}: kernel {kern_cold:.4f} ms per launch; warm-input and per-launch rounds")
     kern_warm = kernel_ms(False, key="warm")
     kern_cold_pair = kernel_ms(True, per_launch=True, key="cold_event_pair_per_launch")
     # the other arithmetic mode of the same shape on the same box, when it has its own kernel
@@ -771,6 +786,7 @@ def main():
     if c4_one:
         out["c4_one_gpu"] = c4_one
     if world == 1 and not args.no_cpu:
+        progress(f"{cfg}: CPU baseline and whole-batch parity")
         out["cpu_baseline"] = cpu_baseline(pr, args.cpu_seconds, args.layout, gpu_sample)
     print(json.dumps(out), flush=True)
     if dist:

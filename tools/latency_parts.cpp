@@ -15,9 +15,12 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <string>
 #include <vector>
 
 #include "qpgpu.h"
+
+extern "C" void qpgpu_debug_set_zero_copy(int64_t bytes);
 
 static double p50(std::vector<double> v) {
   std::sort(v.begin(), v.end());
@@ -169,6 +172,8 @@ int main(int argc, char** argv) {
   const double k_zin = kev_of(zG, zg0, zCE, zce0, zCI, zci0, dx, df, dst);
   const double k_zout = kev_of(dG, dg0, dCE, dce0, dCI, dci0, zx, zf, const_cast<int32_t*>(zst));
   const double k_zboth = kev_of(zG, zg0, zCE, zce0, zCI, zci0, zx, zf, const_cast<int32_t*>(zst));
+  const int zc_status = *zst;
+  const double zc_f = *zf;
   // host to host: pack inputs into the pinned buffer, launch on zero-copy pointers, poll status
   const double poll_both = timeit([&] {
     std::memcpy(zin, pin, inb);
@@ -192,11 +197,65 @@ int main(int argc, char** argv) {
     }
   });
   (void)hipStreamSynchronize(stream);
+  // the host entry per shape, zero-copy (the library's default for small calls) and copies
+  std::string shapes_json;
+  for (int sh = 0; sh < 4; ++sh) {
+    const int N = sh == 0 ? 7 : (sh == 1 ? 14 : (sh == 2 ? 30 : 8)), P = sh == 0 ? 6 : (sh == 1 ? 10 : (sh == 2 ? 6 : 0)),
+              Mm = sh == 0 ? 14 : (sh == 1 ? 28 : (sh == 2 ? 60 : 16));
+    std::vector<double> sG(N * N), sg0(N), sCE(N * P), sce0(P), sCI(N * Mm), sci0(Mm), sx(N), sxf(N), sM(N * N);
+    for (auto& v : sM) v = u();
+    for (int i = 0; i < N; ++i)
+      for (int j = 0; j < N; ++j) {
+        double a = (i == j) ? N : 0.0;
+        for (int k = 0; k < N; ++k) a += sM[k * N + i] * sM[k * N + j];
+        sG[i * N + j] = a;
+      }
+    for (auto& v : sg0) v = 10 * u();
+    for (auto& v : sxf) v = 0.1 * u();
+    for (auto& v : sCE) v = u();
+    for (auto& v : sCI) v = u();
+    for (int k = 0; k < P; ++k) {
+      double a = 0;
+      for (int i = 0; i < N; ++i) a += sCE[i * P + k] * sxf[i];
+      sce0[k] = -a;
+    }
+    for (int k = 0; k < Mm; ++k) {
+      double a = 0;
+      for (int i = 0; i < N; ++i) a += sCI[i * Mm + k] * sxf[i];
+      sci0[k] = -a + std::fabs(u());
+    }
+    qpgpu_problem_desc sd{};
+    sd.n = N;
+    sd.p = P;
+    sd.m = Mm;
+    sd.batch = 1;
+    sd.flags = QPGPU_FLAG_WRITE_FACTOR;  // as the drop-in calls it
+    double sf[2];
+    int32_t sst[2], sit[2];
+    double t_mode[2];
+    double fz[2];
+    for (int zc = 0; zc < 2; ++zc) {
+      qpgpu_debug_set_zero_copy(zc ? (64 << 10) : 0);
+      t_mode[zc] = timeit([&] {
+        std::vector<double> Gc(sG);
+        if (qpgpu_solve_batched_host(&sd, Gc.data(), sg0.data(), sCE.data(), sce0.data(), sCI.data(),
+                                     sci0.data(), sx.data(), sf, sst, sit) != QPGPU_SUCCESS)
+          std::exit(1);
+      });
+      fz[zc] = sf[0];
+    }
+    qpgpu_debug_set_zero_copy(64 << 10);
+    char buf[256];
+    std::snprintf(buf, sizeof buf, "%s\"(%d,%d,%d)\": {\"copies\": %.2f, \"zero_copy\": %.2f, \"same_f\": %s}",
+                  sh ? ", " : "", N, P, Mm, t_mode[0], t_mode[1], fz[0] == fz[1] ? "true" : "false");
+    shapes_json += buf;
+  }
+  std::printf("{\"host_entry_by_shape\": {%s}}\n", shapes_json.c_str());
   std::printf("{\"what\": \"one C1 QP, p50 host-clock us (kernel_*: device clock)\", \"reps\": %d, "
               "\"host_entry\": %.2f, \"solve_dev\": %.2f, \"h2d\": %.2f, \"d2h\": %.2f, \"sync_idle\": %.2f, "
               "\"kernel_ev\": %.2f, \"kernel_zc_in\": %.2f, \"kernel_zc_out\": %.2f, \"kernel_zc_both\": %.2f, "
-              "\"zc_both_poll\": %.2f, \"zc_both_sync\": %.2f, \"h2d_zc_out_poll\": %.2f, \"status\": %d, \"f\": %.17g}\n",
+              "\"zc_both_poll\": %.2f, \"zc_both_sync\": %.2f, \"h2d_zc_out_poll\": %.2f, \"status\": %d, \"f\": %.17g, \"zc_status\": %d, \"zc_f\": %.17g}\n",
               reps, host_entry, solve_dev, h2d, d2h, sync_idle, p50(kev), k_zin, k_zout, k_zboth, poll_both,
-              sync_both, h2d_poll, st, f);
+              sync_both, h2d_poll, st, f, zc_status, zc_f);
   return 0;
 }

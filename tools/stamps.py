@@ -20,7 +20,7 @@ family = sys.argv[4] if len(sys.argv) > 4 else "lane"  # "pair": 32 QPs per wave
 QPW = 32 if family == "pair" else 64
 if kind == "box":
     p = 0
-B = 65536
+B = int(os.environ.get("STAMPS_B", "65536"))  # e.g. 1: one QP (BASELINE config 1 latency)
 pr = qpgpu.make_problems(kind, n, p, m, 0, B, seed=2026)
 db = qpgpu.DeviceBatch(pr, "cuda:0", layout=layout)
 waves = (B + QPW - 1) // QPW
@@ -33,7 +33,8 @@ for rep in range(3):
     torch.cuda.synchronize()
 fn(None)
 s = st.cpu().numpy().reshape(waves, 18).astype(np.int64)
-it = db.iters.cpu().numpy()[: waves * QPW].reshape(waves, QPW)
+itv = db.iters.cpu().numpy()
+it = np.pad(itv, (0, max(0, waves * QPW - len(itv))))[: waves * QPW].reshape(waves, QPW)
 names = ["loads+setup", "equality", "active-set", "stores"]
 tot = s[:, 4] - s[:, 0]
 print(f"{kind} {layout}{' fast' if fast else ''} {family}: total cycles/wave mean {tot.mean():.0f} p50 {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max()}")
@@ -71,6 +72,6 @@ if (rt1 > rt0).all():
     print(f"  wave end   (us after the first start): p50 {np.median(en_us):.2f} p90 {np.percentile(en_us, 90):.2f} max {en_us.max():.2f}")
     dur = en_us - st_us
     print(f"  wave duration us: mean {dur.mean():.2f} p50 {np.median(dur):.2f} max {dur.max():.2f}")
-    for x in range(8):
+    for x in range(8 if waves >= 8 else 0):
         sel = (np.arange(waves) % 8) == x
         print(f"    block%8={x}: start max {st_us[sel].max():.2f} end max {en_us[sel].max():.2f} clock {ghz[sel].mean():.3f}")
