@@ -1259,6 +1259,38 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
       }
       if (lead) ctl->ngiv = ng;
       return true;
+    } else if constexpr (GJR && S == 4 * 64) {
+      // tolerance mode of the workspace variant: the same prefix sum of squares over the block
+      // (a scan per wave, then the waves' totals in wave order), so the |h| chain — n-1-iq
+      // dependent hypots on the lead, 7 % of the C5 loop (profiles/r06_s3) — becomes one scan and
+      // one square root per lane.  A possibly skipped first step (h < 2 eps) or squares outside
+      // [2^-600, 2^600] take the serial chain, as in the fast build.
+      if (!pre) return false;
+      const int ng = iq < n - 1 ? n - 1 - iq : 0;
+      const int g = ls;
+      const double ag = g < ng ? dv[n - 2 - g] : 0.0;
+      double v = ag * ag;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double t = __shfl_up(v, o, 64);
+        v += (ls & 63) >= o ? t : 0.0;
+      }
+      double* const W = Q + Ly.off_tsc;  // (not live between the d/z passes)
+      if ((ls & 63) == 63) W[ls >> 6] = v;
+      __syncthreads();
+      const double d0 = ng > 0 ? dv[n - 1] : 0.0;
+      double P = d0 * d0;
+      for (int w = 0; w < (ls >> 6); w++) P += W[w];
+      P += v;
+      const bool bad = g < ng && (!(P >= 0x1p-600 && P <= 0x1p600) || (g == 0 && P < 4.0 * kEps * kEps) ||
+                                  !(fabs(ag) <= 0x1p300));
+      if (__syncthreads_or(bad)) return false;  // this QP takes the serial chain
+      if (g < ng) {
+        GX_(g) = sqrt(P);
+        GF_(g) = 1.0;
+      }
+      if (lead) ctl->ngiv = ng;
+      return true;
     } else {
       return false;
     }

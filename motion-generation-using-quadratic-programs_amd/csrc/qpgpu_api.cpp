@@ -364,9 +364,11 @@ static constexpr size_t kStagedBytes = 4u << 20;
 // Batches up to g_zero_copy_bytes (a few dozen C1 QPs; one drop-in solve_quadprog() call is 2 KB)
 // skip both copies: the kernel reads its inputs from, and writes its outputs to, the pinned
 // staging buffer itself (mapped host memory), and the call synchronises the stream once.
-// Measured for one C1 QP (profiles/r06_s4/latency.log, tools/latency_parts.cpp): kernel 25.0 us
-// on device-memory inputs against 11.2 us on the mapped buffer, host to host 37.7 us with the
-// copies against 20.1 us without them.
+// Measured per shape, host to host with the factor written
+// back as the drop-in asks (profiles/r06_s6/latency_parts.log, copies -> zero-copy): (7, 6, 14)
+// 42.6 -> 38.6 us, (14, 10, 28) 85.3 -> 82.0, (30, 6, 60) 214.1 -> 208.2, but (8, 0, 16)
+// 61.2 -> 65.1: without an equality phase the first l1 scan waits on the host-memory reads of CI
+// at once, so p = 0 calls keep the copies.
 static size_t g_zero_copy_bytes = 64u << 10;  // kZeroCopyBytes; qpgpu_debug_set_zero_copy
 
 struct PinnedStage {
@@ -458,7 +460,7 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const doubl
     // f | status | iters poisoned (NaN, -1, -1) and sent with the inputs: outputs a kernel did
     // not write never come back as the previous call's values from the reused device buffer
     std::memset(h + of, 0xFF, total - of);
-    if (total <= g_zero_copy_bytes) {
+    if (total <= g_zero_copy_bytes && d->p > 0) {
       // zero-copy: the kernel works on the mapped staging buffer directly
       auto Hp = [&](size_t off) { return reinterpret_cast<double*>(h + off); };
       rc = qpgpu_solve_batched(d, Hp(oG), Hp(og0), Hp(oCE), Hp(oce0), Hp(oCI), Hp(oci0), Hp(ox), Hp(of),

@@ -121,7 +121,7 @@ int main(int argc, char** argv) {
     (void)hipStreamSynchronize(stream);
   });
   const double d2h = timeit([&] {
-    (void)hipMemcpyAsync(hp, dx, 8 * (n + 4), hipMemcpyDeviceToHost, stream);
+    (void)hipMemcpyAsync(hp + inb, dx, 8 * (n + 4), hipMemcpyDeviceToHost, stream);  // (past the inputs)
     (void)hipStreamSynchronize(stream);
   });
   const double sync_idle = timeit([&] { (void)hipStreamSynchronize(stream); });
