@@ -7,6 +7,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <condition_variable>
 #include <cstring>
 #include <functional>
@@ -202,7 +203,7 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
                               const double* CE, const double* ce0, const double* CI,
                               const double* ci0, double* x, double* f, int32_t* status,
                               int32_t* iters, double* x_eq, double* f_eq, int32_t* st_eq,
-                              void* stream);
+                              void* stream, uint32_t internal = 0);
 
 int qpgpu_solve_batched(const qpgpu_problem_desc* d, double* G, const double* g0,
                         const double* CE, const double* ce0, const double* CI,
@@ -226,7 +227,7 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
                               const double* CE, const double* ce0, const double* CI,
                               const double* ci0, double* x, double* f, int32_t* status,
                               int32_t* iters, double* x_eq, double* f_eq, int32_t* st_eq,
-                              void* stream) {
+                              void* stream, uint32_t internal) {
   int rc = validate(d);
   if (rc) return rc;
   if (d->batch == 0) return QPGPU_SUCCESS;
@@ -259,7 +260,7 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
   int handled = 0;
   hipError_t e = hipSuccess;
   std::unique_lock<std::mutex> ws_hold;  // the workspace cache's lock, once a workspace is taken
-  a.flags = d->flags & (QPGPU_FLAG_WRITE_FACTOR | QPGPU_FLAG_EXACT);
+  a.flags = (d->flags & (QPGPU_FLAG_WRITE_FACTOR | QPGPU_FLAG_EXACT)) | internal;
   const bool fast = (d->flags & QPGPU_FLAG_FAST) != 0;
   auto launch_lane = [&]() {
     return fast ? qpk_launch_lane_fast(&a, s, &handled, nullptr) : qpk_launch_lane(&a, s, &handled, nullptr);
@@ -350,6 +351,13 @@ static bool family_covers(uint32_t flags, int n, int p, int m) {
   return qpgpu_kernel_name(n, p, m)[0] != 0;
 }
 
+// Does the launch for these flags run the lane kernel (whose zero-copy stores end with the status
+// word behind a system-scope fence)?
+static bool family_poll(uint32_t flags, int n, int p, int m) {
+  if (flags & (QPGPU_FLAG_FORCE_SUBGROUP | QPGPU_FLAG_FORCE_WAVE | QPGPU_FLAG_FORCE_GENERIC)) return false;
+  return qpk_lane_name(n, p, m) != nullptr;
+}
+
 // Host-pointer entry (the drop-in's path, one QP per solve_quadprog() call, and the batched
 // controller's).  Device buffers are one allocation per thread, laid out
 //   [G | g0 | CE | ce0 | CI | ci0 | x || f | status | iters]
@@ -364,7 +372,9 @@ static constexpr size_t kStagedBytes = 4u << 20;
 // Batches up to g_zero_copy_bytes (a few dozen C1 QPs; one drop-in solve_quadprog() call is 2 KB)
 // skip both copies: the kernel reads its inputs from, and writes its outputs to, the pinned
 // staging buffer itself (mapped host memory), and the call synchronises the stream once.
-// Measured per shape, host to host with the factor written
+// With the status-word poll below, one C1 call is 34.5 us host to host (41.3 with the copies;
+// profiles/r06_s11/latency_parts.log) and one drop-in solve_quadprog() 34.7 us p50 (39.9 in round
+// 5).  Measured per shape before the poll, host to host with the factor written
 // back as the drop-in asks (profiles/r06_s6/latency_parts.log, copies -> zero-copy): (7, 6, 14)
 // 42.6 -> 38.6 us, (14, 10, 28) 85.3 -> 82.0, (30, 6, 60) 214.1 -> 208.2, but (8, 0, 16)
 // 61.2 -> 65.1: without an equality phase the first l1 scan waits on the host-memory reads of CI
@@ -463,13 +473,32 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const doubl
     if (total <= g_zero_copy_bytes && d->p > 0) {
       // zero-copy: the kernel works on the mapped staging buffer directly
       auto Hp = [&](size_t off) { return reinterpret_cast<double*>(h + off); };
-      rc = qpgpu_solve_batched(d, Hp(oG), Hp(og0), Hp(oCE), Hp(oce0), Hp(oCI), Hp(oci0), Hp(ox), Hp(of),
-                               reinterpret_cast<int32_t*>(h + os), reinterpret_cast<int32_t*>(h + oi), s);
+      // The lane kernel (n <= 8, m <= 16) stores x, f and iters, then a system-scope fence,
+      // then the status word (qpk::kArgHostPoll): the host spins on the status words it
+      // poisoned instead of waiting for the stream's completion signal (~5 us of a single call).
+      // Other kernels, and a kernel that ends without writing them, take the stream sync.
+      const bool poll = family_poll(d->flags, d->n, d->p, d->m);
+      volatile int32_t* const hst = reinterpret_cast<volatile int32_t*>(h + os);
+      rc = solve_batched_impl(d, Hp(oG), Hp(og0), Hp(oCE), Hp(oce0), Hp(oCI), Hp(oci0), Hp(ox), Hp(of),
+                              reinterpret_cast<int32_t*>(h + os), reinterpret_cast<int32_t*>(h + oi),
+                              nullptr, nullptr, nullptr, s, poll ? qpk::kArgHostPoll : 0u);
       if (rc) {
         (void)hipStreamSynchronize(s);
         return rc;
       }
-      if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+      bool done = false;
+      if (poll) {
+        for (long spin = 0; !done; ++spin) {
+          done = true;
+          for (size_t b = 0; b < B && done; b++) done = hst[b] != -1;
+          if (!done && (spin & 4095) == 4095) {
+            e = hipStreamQuery(s);  // finished without writing, or failed: leave to the sync below
+            if (e != hipErrorNotReady) break;
+          }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+      }
+      if (!done && (e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
       std::memcpy(x, h + ox, nx);
       std::memcpy(f, h + of, nf);
       std::memcpy(status, h + os, ns);

@@ -52,6 +52,21 @@ def main():
     pair = "qp_pair" in kname
     fe = per_kernel(fetch_dir, "FETCH_SIZE", fast, pair)
     wr = per_kernel(write_dir, "WRITE_SIZE", fast, pair)
+    # the n > 64 default runs the workspace kernel twice per step: the tolerance loop, then the
+    # certification's EXACT re-solve, whose workgroups exit at once unless their QP is marked
+    #  — the same kernel name with a tiny count; its dispatches are split off
+    def split(vals):
+        out = {}
+        for k, v in vals.items():
+            top = max(v) if v else 0.0
+            big = [x for x in v if x >= 0.01 * top]
+            small = [x for x in v if x < 0.01 * top]
+            out[k] = big
+            if small and big:
+                out[k + " [re-solve launch]"] = small
+        return out
+
+    fe, wr = split(fe), split(wr)
     kernels = {}
     for k in sorted(set(fe) | set(wr)):
         fk = statistics.median(fe[k]) if fe[k] else 0.0
