@@ -96,6 +96,8 @@ constexpr int kScanDepth = 2;
 // first scan load them (0).  Measured on C2 (profiles/r03_s6): 83.6 us with the DMA, 72.9 without
 // — the DMA's per-lane 16-B pieces take ~23k cycles per wave to issue, the first scan's direct
 // loads 18.5k, and nothing hides either — so 0; with p > 0 the equality phase hides the DMA.
+// 2: a part per Cholesky row (profiles/r06_s15: 75.2 us per launch against 67.6-68.0 with 0,
+// pipelined 1.489e9 against 1.449e9 solves/s — an A/B value, not the default).
 #ifndef QPGPU_LANE_DMA_P0
 #define QPGPU_LANE_DMA_P0 0
 #endif
@@ -321,6 +323,10 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
 #pragma unroll
     for (int i = 0; i < NM; i++) {
       round_b(i, NM);  // every lane (the copy is per wave)
+      // p = 0 (no round B, no equality phase): the CI copy a part per Cholesky row instead
+      // (QPGPU_LANE_DMA_P0 = 2; G has left the LDS for registers at the barrier above)
+      if constexpr (kCiDma && PX == 0 && QPGPU_LANE_DMA_P0 == 2)
+        if (dma) dma_ci_part(i, NM);
       if (i < n && chol_ok) {
         double sum = Gr[i][i];
 #pragma unroll
@@ -466,7 +472,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
     // no equality phase to hide the copy behind: issued after the setup, all at once (the first
     // scan waits for it either way; during the Cholesky its issue stalls the setup's compute)
     if (dma) {
-      dma_ci_part(0, 1);
+      if constexpr (QPGPU_LANE_DMA_P0 != 2) dma_ci_part(0, 1);
       warmup();
     }
   }
