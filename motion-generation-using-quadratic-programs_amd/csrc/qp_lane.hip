@@ -87,7 +87,14 @@ __device__ __forceinline__ double from_agpr(const AgprD& a) {
 }
 
 constexpr int kQpw = 64;      // QPs per wave: one per lane
-constexpr int kStage = 5120;  // staging buffer, doubles (40 KiB: 4 waves per CU)
+// Two waves per SIMD (QPGPU_LANE_OCC2, an A/B build for VERDICT r05 item 6): 256 registers per
+// lane and a 20 KiB stage (eight waves per CU); G and CE no longer stage, each lane loads its own
+// from global memory, and the LDS copy of CI shrinks to the rows the smaller stage holds.
+#ifndef QPGPU_LANE_OCC2
+#define QPGPU_LANE_OCC2 0
+#endif
+constexpr int kLaneOcc = QPGPU_LANE_OCC2 ? 2 : 1;
+constexpr int kStage = QPGPU_LANE_OCC2 ? 2560 : 5120;  // staging buffer, doubles (40 KiB: 4 waves per CU)
 // The first l1 scan (which fills the on-chip CI copy) is software-pipelined two rows deep: row
 // j+1's loads are issued (and fenced from the scheduler) before row j is consumed, so one memory
 // latency covers two rows instead of the scheduler's one-load-at-a-time minimum-pressure order.
@@ -207,7 +214,9 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
   // then rows 0..kCiRows-1 of every lane's CI for the active-set loop (16-B pieces, piece k of
   // lane l at doubles (k*64 + l)*2).  RB, at the top, stages g0.
   constexpr int RB = (STAGE - kQpw * NM) / 2 * 2;
-  static_assert(RB >= kQpw * NM * NM, "G and g0 staging exceed the stage buffer");
+  // G and g0 stage through LDS when they fit (the product); else each lane loads its own
+  constexpr bool kStageG = RB >= kQpw * NM * NM;
+  static_assert(kStageG || QPGPU_LANE_OCC2, "G and g0 staging exceed the stage buffer");
   // CI rows held in LDS through the loop (EXACT QP-major shapes)
   constexpr int kCiRowsFit = (RB / kQpw) / MM;
   constexpr int kCiRows = (EXACT && T == 1 && MM % 2 == 0) ? (kCiRowsFit < NM ? kCiRowsFit : NM) : 0;
@@ -270,8 +279,10 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
     double Gr[NM][NM];
     // round A: G and g0
     const int offg0 = RB;
-    stage_all(a.G, n * n, 0);
-    stage_all(a.g0, n, offg0);
+    if constexpr (kStageG) {
+      stage_all(a.G, n * n, 0);
+      stage_all(a.g0, n, offg0);
+    }
     __syncthreads();
     // The LDS reads are unconditional (in range for every lane; an idle lane's slot holds stale
     // data that the select drops): a read under `live` becomes one exec-masked block per element,
@@ -281,10 +292,18 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
     for (int i = 0; i < NM; i++) {
 #pragma unroll
       for (int j = 0; j < NM; j++) {
-        const double v = (i < n && j < n) ? rd_all(0, n * n, i * n + j) : 0.0;
+        double v;
+        if constexpr (kStageG)
+          v = (i < n && j < n) ? rd_all(0, n * n, i * n + j) : 0.0;
+        else
+          v = (live && i < n && j < n) ? view(const_cast<double*>(a.G), n * n)[(i * n + j) * T] : 0.0;
         Gr[i][j] = live ? v : 0.0;
       }
-      const double v0 = i < n ? rd_all(offg0, n, i) : 0.0;
+      double v0;
+      if constexpr (kStageG)
+        v0 = i < n ? rd_all(offg0, n, i) : 0.0;
+      else
+        v0 = (live && i < n) ? view(const_cast<double*>(a.g0), n)[i * T] : 0.0;
       g0v[i] = live ? v0 : 0.0;
     }
     __syncthreads();
@@ -1232,7 +1251,7 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
 }
 
 template <int NM, int MM, int T, bool EXACT, int PX>
-__global__ void __launch_bounds__(64, 1) QP_LANE_KERNEL(const QpArgs a) {
+__global__ void __launch_bounds__(64, kLaneOcc) QP_LANE_KERNEL(const QpArgs a) {
   __shared__ double sbuf[kStage];
   if constexpr (kFast) {
     if (!lane_body<NM, MM, T, EXACT, PX, false>(a, sbuf)) {
