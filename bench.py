@@ -78,7 +78,9 @@ def arithmetic_of(kname):
         return ("fast (opt-in): fused multiply-adds, shared reciprocals; x within 1e-10 relative, "
                 "f within 1e-10 of its terms (not north_star's plain f bar, DESIGN 3.3)")
     if "qp_panel" in kname:
-        return ("tolerance, certified: MFMA panel setup + tree-summed loop sums (n > 64 default), "
+        return ("tolerance, certified: MFMA panel setup + tree-summed loop sums (n > 64 default; l1 "
+                "scans filtered through an fp32 copy of CI with rigorous bounds, fp64 sums for the "
+                "constraints the select can pick), "
                 "every QP whose decisions that arithmetic cannot certify re-solved in the "
                 "reference's order (certification); status and l1 passes identical, x, f within "
                 "north_star's plain 1e-10 relative per QP on any input (cpu_baseline.parity over "
@@ -138,6 +140,8 @@ def parse(argv=None):
                          "3.3); the default line reports it beside the bitwise build")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-shadow", action="store_true",
+                    help="A/B: n > 64 default path's l1 scans in fp64 only (no fp32 copy of CI)")
     ap.add_argument("--no-c4", action="store_true", help="skip the N = 1 line's C4-on-one-GPU record")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--ops-json", default=os.path.join(ROOT, "profiles", "op_counts.json"))
@@ -349,6 +353,8 @@ def main():
 
     cfg = args.config or ("C1" if world == 1 else "C4")
     kind, n, p, m, bdef, desc = CONFIGS[cfg]
+    if args.no_shadow:
+        qpgpu.set_shadow(False)
     if args.kernel_reps is None:
         args.kernel_reps = 3 if cfg == "C5" else 20
     if args.kernel_rounds is None:
@@ -646,9 +652,14 @@ def main():
     if "qp_panel" in kname and not args.family:
         qpgpu.set_resolve(False)
         try:
+            qpgpu.shadow_stats(reset=True)
             hb.launcher(cs)()
             torch.cuda.synchronize(dev)
+            tried, settled = qpgpu.shadow_stats(reset=True)
             cert = {"qps": B, "marked_for_exact_resolve": qpgpu.unc_reasons(hb.status[:B].cpu().numpy()),
+                    "l1_scans": {"from_fp32_copy_tried": tried, "settled_by_its_bounds": settled,
+                                 "note": "DESIGN §6.7: the other scans (and every scan with --no-shadow) "
+                                         "read CI in fp64"},
                     "note": "QPs the tolerance mode cannot certify (a near-dependent add, a decision "
                             "within its rounding margin, cancellation, a failed or badly spread "
                             "setup) are re-solved in the reference's order by a third launch of "
@@ -757,7 +768,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": desc, "kind": kind, "n": n, "p": p, "m": m, "batch_per_gpu": B,
                    "global_batch": B * world, "kernel": kname, "layout": args.layout,
-                   "arithmetic": arithmetic_of(kname),
+                   "arithmetic": arithmetic_of(kname) + (" [A/B: fp64-only l1 scans]" if args.no_shadow else ""),
                    "streams": S, "input_sets": R, "cold_inputs": R > 1 or in_bytes * B >= 2 * MALL_BYTES,
                    "backend": backend if world > 1 else None, "parallelism": par},
         "per_gpu_batch": B,

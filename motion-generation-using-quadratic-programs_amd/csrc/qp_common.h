@@ -351,6 +351,9 @@ constexpr uint32_t kArgHostPoll = 0x10000000u;
 // internal QpArgs.flags bit: the EXACT re-solve launch after a tolerance-mode launch — only the
 // QPs whose status carries kStResolve are solved (one QP per workgroup: the others exit at once)
 constexpr uint32_t kResolveOnly = 0x20000000u;
+// internal QpArgs.flags bit: the workspace holds an fp32 copy of CI after the batch's per-QP
+// blocks (qp_wave.hip qp_ci_shadow_kernel), which the tolerance-mode l1 scan reads first
+constexpr uint32_t kArgShadow = 0x08000000u;
 // Tolerance mode (n > 64 default: MFMA panel setup + tree sums) certification.  A QP one of whose
 // decisions the tolerance arithmetic cannot certify against the reference's rounding is marked in
 // its status word (kStResolve | reason << kStReasonShift) and re-solved by the EXACT launch, which

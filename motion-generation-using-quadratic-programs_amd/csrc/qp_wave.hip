@@ -327,6 +327,23 @@ __device__ __forceinline__ double colsum16(double (&v)[16]) {
 #ifndef QPGPU_WAVE_STAMPS_DETAIL
 #define QPGPU_WAVE_STAMPS_DETAIL 0
 #endif
+// Tolerance-mode l1 scan from an fp32 copy of CI (the workspace variant, n > 64):
+// each s_i first from the half-size copy with a rigorous bound on its distance from the fp64
+// sum, then the exact fp64 sum only for the constraints the select can pick; a pass whose stop
+// test or candidates the bounds cannot settle scans in fp64 as before.  0 = always fp64.
+#ifndef QPGPU_WAVE_SHADOW
+#define QPGPU_WAVE_SHADOW 1
+#endif
+constexpr int kShadowCand = 16;  // most exact re-evaluations per shadow scan (else the fp64 scan)
+// diagnostic counts (qpgpu_debug_shadow_stats): l1 scans that tried the fp32 copy, and those the
+// bounds settled (one atomic per QP and scan, by the lead)
+__device__ unsigned long long g_shadow_stats[2];
+#ifndef QPGPU_WAVE_SHADOW_U  // fp32 CI loads per constraint and chunk of the shadow scan
+#define QPGPU_WAVE_SHADOW_U 32
+#endif
+#ifndef QPGPU_WAVE_SHADOW_KP  // a lane's constraints whose chunks load together
+#define QPGPU_WAVE_SHADOW_KP 1
+#endif
 // per-QP control block (lead lane writes, subgroup reads after grp_sync)
 struct Ctl {
   double f, t, t1, t2, ss, R_norm, c1, c2, psi, ci0ip, znp;
@@ -369,7 +386,7 @@ struct WaveCfg {
 constexpr int kTolCh = QPGPU_WAVE_TOLCH;  // columns per tree-summed chunk of the tolerance-mode d/z pass
 struct WaveLay {
   int js, nr, off_r, off_x, off_z, off_d, off_np, off_rv, off_xo, off_gc, off_u, off_uo, off_s,
-      off_a, off_fl, off_ctl, off_tsc, stride;
+      off_a, off_fl, off_ctl, off_tsc, off_sp, stride;
 };
 __host__ __device__ inline WaveLay wave_lay(int n, int m, bool gjr, bool rpack = false) {
   WaveLay L;
@@ -411,7 +428,10 @@ __host__ __device__ inline WaveLay wave_lay(int n, int m, bool gjr, bool rpack =
   }
   // the workspace variant's tolerance-mode partial sums (two buffers of 4 waves x kTolCh)
   L.off_tsc = L.off_ctl + (int)((sizeof(Ctl) + 7) / 8);
-  L.stride = (L.off_tsc + (gjr ? 2 * 4 * kTolCh : 0)) | 1;
+  // the workspace variant's shadow scan: the n products of one exact re-evaluation, then the
+  // candidate list (kShadowCand ints) and its count
+  L.off_sp = L.off_tsc + (gjr ? 2 * 4 * kTolCh : 0);
+  L.stride = (L.off_sp + (gjr ? n + kShadowCand / 2 + 1 : 0)) | 1;
   return L;
 }
 // packed-R index: R[i][j] for j >= i, the subdiagonal R[j+1][j], else a write-only slot (the
@@ -1767,6 +1787,197 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
     grp_sync<S>();
   }
   // ------------------------------------------------------------------ active-set loop
+  // ---- the tolerance-mode l1 scan from the fp32 copy of CI (QPGPU_WAVE_SHADOW; workspace
+  // variant).  Each lane's s~_i = fl(sum_j (double)CI32[j][i] x_j) + ci0_i in j order, with a bound
+  // B_i >= |s_i - s~_i| for the fp64 scan's s_i: CI32 = CI (1 + d), |d| <= 2^-24, or |CI32 - CI|
+  // <= 2^-126 below fp32's normal range, and both sums' rounding (each <= (n + 1) eps' of
+  // sum |CI_ij x_j| + |ci0_i|), and products below the normal range — B_i = 1.001 (5.97e-8 A_i +
+  // 2e-38 sum|x| + 1e-13 |ci0_i|) + 1e-300, A_i = sum |CI32_ij x_j|.  Accepted (true) only when
+  //   * every s~_i and B_i is finite,
+  //   * |psi~| - E > 1.001 thr + 1e-10 sigma_s m, where psi~ sums the negative s~_i and E bounds
+  //     |psi - psi~| (1.001 x the B_i of every constraint that may be negative, plus both sums'
+  //     rounding, 4e-16 m sum |s~_i| over them): the fp64 psi then continues the loop and stays
+  //     outside kUncPsi's window;
+  //   * at most kShadowCand constraints are candidates: not active, lower bound below 0 and not
+  //     above H2, the second-smallest upper bound among those — the two smallest fp64 values are
+  //     among them, so the select's pick, its runner-up (kUncSelTie) and any re-select after a
+  //     degenerate add (which compares against the carried ss, itself a candidate's value) come
+  //     out as from the fp64 scan, the other s~_i lying above every value they are compared with.
+  // The candidates get their fp64 s_i (the same products and the same j-order sum as the fp64
+  // scan: the lanes form the n products, the lead adds them) into sv; the other sv entries keep
+  // s~_i.  Otherwise (false) the caller scans in fp64, overwriting sv.
+  constexpr bool kShadow = GJR && QPGPU_WAVE_SHADOW && S == 4 * 64 && NMAX <= S;
+  bool shadow_hit = false;
+  [[maybe_unused]] auto shadow_scan = [&]() -> bool {
+    constexpr int KS = (MMAX + S - 1) / S;  // constraints per lane
+    const float* const C32 = reinterpret_cast<const float*>(ws + a.batch * (int64_t)C::WS_DOUBLES) + bb * (int64_t)n * m;
+    double* const W = Q + Ly.off_tsc;  // (not live between the d/z passes)
+    double* const P = Q + Ly.off_sp;
+    int* const cl = reinterpret_cast<int*>(P + n);  // [0] count, [1..kShadowCand] candidates
+    if (lead) cl[0] = 0;
+    double bk[KS];  // (s~_i is read back from sv)
+    double lpsi = 0.0, le = 0.0, les = 0.0;
+    bool lbad = false;
+    // KP of a lane's constraints per pass over j (their loads of a chunk in flight together)
+    constexpr int KP = QPGPU_WAVE_SHADOW_KP < KS ? QPGPU_WAVE_SHADOW_KP : KS;
+    static_assert(KS % KP == 0, "constraints per lane in whole groups");
+#pragma unroll
+    for (int k0 = 0; k0 < KS; k0 += KP) {
+      if (ls + k0 * S < m) {
+        double sa[KP], Aa[KP], X = 0.0;
+        int ia[KP];
+#pragma unroll
+        for (int q = 0; q < KP; q++) {
+          sa[q] = 0.0;
+          Aa[q] = 0.0;
+          ia[q] = ls + (k0 + q) * S < m ? ls + (k0 + q) * S : m - 1;  // (a clamped one is discarded)
+        }
+        constexpr int U = QPGPU_WAVE_SHADOW_U;
+        for (int jb = 0; jb < n; jb += U) {
+          float c[KP][U];
+#pragma unroll
+          for (int q = 0; q < KP; q++)
+#pragma unroll
+            for (int u = 0; u < U; u++) c[q][u] = C32[(jb + u < n ? jb + u : n - 1) * m + ia[q]];
+#pragma unroll
+          for (int u = 0; u < U; u++)
+            if (jb + u < n) {
+              const double xj = xv[jb + u];
+              X += fabs(xj);
+#pragma unroll
+              for (int q = 0; q < KP; q++) {
+                const double cd = (double)c[q][u];
+                sa[q] += cd * xj;
+                Aa[q] += fabs(cd) * fabs(xj);
+              }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < KP; q++) {
+          const int i = ls + (k0 + q) * S;
+          bk[k0 + q] = 0.0;
+          if (i < m) {
+            const double c0 = EL(ci0b, i);
+            const double s = sa[q] + c0;
+            const double B = 1.001 * (5.97e-8 * Aa[q] + 2e-38 * X + 1e-13 * fabs(c0)) + 1e-300;
+            lbad = lbad || !(fabs(s) < inf && B < inf);
+            sv[i] = s;
+            exc[i] = 0;
+            bk[k0 + q] = B;
+            if (s - B < 0.0) {
+              le += B;
+              les += fabs(s);
+            }
+            if (s < 0.0) lpsi += s;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < KP; q++) bk[k0 + q] = 0.0;
+      }
+    }
+    const int w = ls >> 6;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      lpsi += __shfl_xor(lpsi, o, 64);
+      le += __shfl_xor(le, o, 64);
+      les += __shfl_xor(les, o, 64);
+    }
+    const bool wbad = __builtin_amdgcn_ballot_w64(lbad) != 0;
+    if ((ls & 63) == 0) {
+      W[4 * w] = lpsi;
+      W[4 * w + 1] = le;
+      W[4 * w + 2] = les;
+      W[4 * w + 3] = wbad ? 1.0 : 0.0;
+    }
+    grp_sync<S>();
+    double psi = 0.0, E = 0.0, Es = 0.0;
+    bool bad = false;
+#pragma unroll
+    for (int v = 0; v < S / 64; v++) {
+      psi += W[4 * v];
+      E += W[4 * v + 1];
+      Es += W[4 * v + 2];
+      bad = bad || W[4 * v + 3] != 0.0;
+    }
+    const double thr = (double)m * kEps * ctl->c1 * ctl->c2 * 100.0;
+    if (bad || !(fabs(psi) - (1.001 * E + 4e-16 * m * Es) > 1.001 * thr + 1e-10 * sigma_s() * m)) return false;
+    // the two smallest upper bounds among the constraints the select may pick
+    double h1 = inf, h2 = inf;
+#pragma unroll
+    for (int k = 0; k < KS; k++) {
+      const int i = ls + k * S;
+      const double sk = i < m ? sv[i] : 0.0;
+      if (i < m && sk - bk[k] < 0.0 && !act[i]) {
+        const double hi = sk + bk[k];
+        if (hi < h1) {
+          h2 = h1;
+          h1 = hi;
+        } else if (hi < h2) {
+          h2 = hi;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double c1 = __shfl_xor(h1, o, 64), c2 = __shfl_xor(h2, o, 64);
+      if (c1 < h1) {
+        h2 = fmin(h1, c2);
+        h1 = c1;
+      } else {
+        h2 = fmin(h2, c1);
+      }
+    }
+    if ((ls & 63) == 0) {
+      W[16 + 2 * w] = h1;
+      W[17 + 2 * w] = h2;
+    }
+    grp_sync<S>();
+    h1 = W[16];
+    h2 = W[17];
+#pragma unroll
+    for (int v = 1; v < S / 64; v++) {
+      const double c1 = W[16 + 2 * v], c2 = W[17 + 2 * v];
+      if (c1 < h1) {
+        h2 = fmin(h1, c2);
+        h1 = c1;
+      } else {
+        h2 = fmin(h2, c1);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KS; k++) {
+      const int i = ls + k * S;
+      const double sk = i < m ? sv[i] : 0.0;
+      if (i < m && sk - bk[k] < 0.0 && !act[i] && sk - bk[k] <= h2) {
+        const int pos = atomicAdd(&cl[0], 1);
+        if (pos < kShadowCand) cl[1 + pos] = i;
+      }
+    }
+    grp_sync<S>();
+    const int cnt = cl[0];
+    if (cnt > kShadowCand) return false;
+    for (int c = 0; c < cnt; c++) {
+      const int i = cl[1 + c];
+      if (ls < n) P[ls] = EL(CIb, ls * m + i) * xv[ls];
+      grp_sync<S>();
+      if (lead) {
+        double s = 0.0;
+        for (int jb = 0; jb < n; jb += 8) {
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) v[u] = P[jb + u < n ? jb + u : n - 1];
+#pragma unroll
+          for (int u = 0; u < 8; u++)
+            if (jb + u < n) s += v[u];
+        }
+        sv[i] = s + EL(ci0b, i);
+      }
+      grp_sync<S>();
+    }
+    return true;
+  };
+
   // Per-subgroup state machine; a wave loops until all of its QPs are done.
   const int max_steps = a.max_steps;
   // the select that follows a scan (carried ss reset to 0): its argmin, the np gather and
@@ -1876,17 +2087,35 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
           from_scan = true;
         }
       } else {
-        for (int i = ls; i < m; i += S) {
-          const double c0 = EL(ci0b, i);  // issued with the first chunk, added last
-          double s = seq_fma_up<KG>(0.0, 0, n, [&](int j) { return EL(CIb, j * m + i); },
-                                [&](int j) { return xv[j]; });
-          s += c0;
-          sv[i] = s;
-          exc[i] = 0;
+        shadow_hit = false;
+        if constexpr (kShadow) {
+          if (pre && (a.flags & kArgShadow)) {
+            shadow_hit = shadow_scan();
+            if (lead) {
+              atomicAdd(&g_shadow_stats[0], 1ull);
+              if (shadow_hit) atomicAdd(&g_shadow_stats[1], 1ull);
+            }
+          }
+        }
+        if (!shadow_hit) {
+          for (int i = ls; i < m; i += S) {
+            const double c0 = EL(ci0b, i);  // issued with the first chunk, added last
+            double s = seq_fma_up<KG>(0.0, 0, n, [&](int j) { return EL(CIb, j * m + i); },
+                                  [&](int j) { return xv[j]; });
+            s += c0;
+            sv[i] = s;
+            exc[i] = 0;
+          }
         }
       }
       grp_sync<S>();
-      if (lead) {
+      if (lead && shadow_hit) {
+        // the bounds settled the stop test (|psi| is above the threshold and outside the
+        // certification window whatever the fp64 values) and the candidates hold their fp64 s
+        ctl->ss = 0.0;
+        ctl->ip = 0;
+        ctl->phase = PH_SELECT;
+      } else if (lead) {
         double psi = 0.0;
         int negc = 0;  // (certification: the negative s_i psi sums)
         constexpr int U = 8;  // loads of a chunk together, adds in i order
@@ -2409,11 +2638,6 @@ extern "C" const char* qpk_medium_name(int n, int /*p*/, int m) {
 }
 extern "C" int qpk_medium_max_n(void) { return 256; }
 extern "C" int qpk_medium_max_m(void) { return 1024; }
-// bytes of device workspace the medium kernels need for a batch (0 = none)
-extern "C" int64_t qpk_medium_workspace_bytes(int n, int m, int64_t batch) {
-  const qpk::WaveVariant* v = qpk::pick_wave(n, m);
-  return v ? v->ws_doubles_per_qp * 8 * batch : 0;
-}
 extern "C" hipError_t qpk_launch_panel_setup(const qpk::QpArgs* a, hipStream_t stream, double* ws);
 
 // Workspace variants (n > 64) run the MFMA panel setup (qp_panel.hip) first unless the caller
@@ -2424,6 +2648,27 @@ extern "C" hipError_t qpk_launch_panel_setup(const qpk::QpArgs* a, hipStream_t s
 static bool g_resolve = true;
 static bool uses_panel(const qpk::WaveVariant* v, uint32_t flags) {
   return v->ws_doubles_per_qp > 0 && !(flags & (QPGPU_FLAG_EXACT | QPGPU_FLAG_WRITE_FACTOR));
+}
+
+// The fp32 copy of CI for the tolerance-mode shadow scan (QPGPU_WAVE_SHADOW): QP-major batches
+// of the panel path, after the batch's per-QP workspace blocks, up to 16 GiB (a larger batch
+// scans in fp64).  qpk_set_shadow(0) (qpgpu_debug_set_shadow) turns it off for A/B tests.
+static bool g_shadow = QPGPU_WAVE_SHADOW != 0;
+static int64_t shadow_bytes(const qpk::WaveVariant* v, const qpk::QpArgs* a) {
+  if (!g_shadow || !uses_panel(v, a->flags) || a->tile != 1 || a->m <= 0) return 0;
+  const int64_t b = (int64_t)a->n * a->m * 4 * a->batch;
+  return b <= ((int64_t)16 << 30) ? (b + 255) / 256 * 256 : 0;
+}
+__global__ void __launch_bounds__(256) qp_ci_shadow_kernel(const double* __restrict__ ci, float* __restrict__ out,
+                                                           int64_t count) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += stride) out[i] = (float)ci[i];
+}
+
+// bytes of device workspace the medium kernels need for a launch (0 = none)
+extern "C" int64_t qpk_medium_workspace_bytes(const qpk::QpArgs* a) {
+  const qpk::WaveVariant* v = qpk::pick_wave(a->n, a->m);
+  return v ? v->ws_doubles_per_qp * 8 * a->batch + shadow_bytes(v, a) : 0;
 }
 
 extern "C" hipError_t qpk_launch_medium_ws(const qpk::QpArgs* a, hipStream_t stream, int* handled,
@@ -2440,6 +2685,15 @@ extern "C" hipError_t qpk_launch_medium_ws(const qpk::QpArgs* a, hipStream_t str
     if (e != hipSuccess) return e;
     qpk::QpArgs b = *a;
     b.flags |= qpk::kSetupDone;
+    if (shadow_bytes(v, a) > 0) {
+      const int64_t count = (int64_t)a->n * a->m * a->batch;
+      const int64_t want = (count + 255) / 256;
+      const unsigned blocks = (unsigned)(want < 16384 ? want : 16384);
+      hipLaunchKernelGGL(qp_ci_shadow_kernel, dim3(blocks), dim3(256), 0, stream, a->CI,
+                         reinterpret_cast<float*>(ws + a->batch * v->ws_doubles_per_qp), count);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      b.flags |= qpk::kArgShadow;
+    }
     e = v->launch(b, stream, ws);
     if (e != hipSuccess || !g_resolve) return e;
     // the QPs the tolerance mode could not certify (status | kStResolve) again in the reference's
@@ -2453,4 +2707,17 @@ extern "C" hipError_t qpk_launch_medium_ws(const qpk::QpArgs* a, hipStream_t str
 // test / diagnostic hook (qpgpu_debug_set_resolve): 0 leaves the tolerance mode's marks in
 // the status words and skips the EXACT re-solve
 extern "C" void qpk_set_resolve(int on) { g_resolve = on != 0; }
+// test / diagnostic hook (qpgpu_debug_set_shadow): 0 scans in fp64 only
+extern "C" void qpk_set_shadow(int on) { g_shadow = on != 0 && QPGPU_WAVE_SHADOW != 0; }
+// diagnostic (qpgpu_debug_shadow_stats): out[0] scans that tried the fp32 copy, out[1] those it
+// settled, since the last reset; device-synchronous
+extern "C" hipError_t qpk_shadow_stats(unsigned long long* out, int reset) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(qpk::g_shadow_stats), 2 * sizeof(unsigned long long));
+  if (e == hipSuccess && reset) {
+    const unsigned long long z[2] = {0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(qpk::g_shadow_stats), z, sizeof(z));
+  }
+  return e;
+}
 #endif  // QPGPU_WAVE_FAST

@@ -31,7 +31,7 @@ extern "C" hipError_t qpk_launch_lane_fast(const qpk::QpArgs* a, hipStream_t str
 extern "C" const char* qpk_lane_name_fast(int n, int p, int m);
 extern "C" hipError_t qpk_launch_medium_ws(const qpk::QpArgs* a, hipStream_t stream, int* handled,
                                            const char** name, double* ws);
-extern "C" int64_t qpk_medium_workspace_bytes(int n, int m, int64_t batch);
+extern "C" int64_t qpk_medium_workspace_bytes(const qpk::QpArgs* a);
 extern "C" const char* qpk_medium_name(int n, int p, int m);
 extern "C" const char* qpk_medium_name_fast(int n, int p, int m);
 extern "C" int qpk_generic_covers(int n, int m);
@@ -273,7 +273,7 @@ static int solve_batched_impl(const qpgpu_problem_desc* d, double* G, const doub
       if (handled) return QPGPU_SUCCESS;
     }
     double* ws = nullptr;
-    const int wrc = device_workspace(qpk_medium_workspace_bytes(a.n, a.m, a.batch), s, &ws, ws_hold);
+    const int wrc = device_workspace(qpk_medium_workspace_bytes(&a), s, &ws, ws_hold);
     if (wrc) return wrc;
     e = qpk_launch_medium_ws(&a, s, &handled, nullptr, ws);
     return QPGPU_SUCCESS;
@@ -680,6 +680,23 @@ void qpgpu_debug_set_zero_copy(int64_t bytes) { g_zero_copy_bytes = bytes > 0 ? 
 // QPs its tolerance mode did not certify, leaving their marks (0x100 | reasons << 9) in status.
 extern "C" void qpk_set_resolve(int on);
 void qpgpu_debug_set_resolve(int on) { qpk_set_resolve(on); }
+
+// Test hook (not in include/qpgpu.h): 0 makes the n > 64 default path's l1 scans fp64-only
+// (no fp32 copy of CI), the A/B side of the shadow scan's bitwise test.
+extern "C" void qpk_set_shadow(int on);
+void qpgpu_debug_set_shadow(int on) { qpk_set_shadow(on); }
+// Diagnostic (not in include/qpgpu.h): out[0] = l1 scans of the n > 64 default path that tried
+// the fp32 copy of CI, out[1] = those its bounds settled, since the last reset (reset != 0
+// zeroes them after reading).  Synchronises the current device.
+extern "C" hipError_t qpk_shadow_stats(unsigned long long* out, int reset);
+int qpgpu_debug_shadow_stats(uint64_t* out, int reset) {
+  unsigned long long v[2] = {0, 0};
+  const hipError_t e = qpk_shadow_stats(v, reset);
+  if (e != hipSuccess) return hip_fail(e, "shadow stats");
+  out[0] = v[0];
+  out[1] = v[1];
+  return QPGPU_SUCCESS;
+}
 
 // Test hook (not in include/qpgpu.h): the generic kernel's per-launch workspace cap in bytes
 // (<= 0 restores the 4 GiB default), so the sub-batch path runs on small shapes.

@@ -169,6 +169,27 @@ def set_resolve(on: bool) -> None:
     fn(1 if on else 0)
 
 
+def set_shadow(on: bool) -> None:
+    """Test / diagnostic hook: False makes the n > 64 default path's l1 scans fp64-only instead of
+    reading the fp32 copy of CI first; results are the same bit for bit."""
+    fn = LIB.qpgpu_debug_set_shadow
+    fn.argtypes = [ctypes.c_int]
+    fn(1 if on else 0)
+
+
+def shadow_stats(reset: bool = True) -> tuple:
+    """(l1 scans of the n > 64 default path that tried the fp32 copy of CI, scans it settled)
+    since the last reset; synchronises the device."""
+    fn = LIB.qpgpu_debug_shadow_stats
+    fn.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    fn.restype = ctypes.c_int
+    out = (ctypes.c_uint64 * 2)()
+    rc = fn(out, 1 if reset else 0)
+    if rc:
+        raise QpgpuError(f"qpgpu_debug_shadow_stats: {rc} {LIB.qpgpu_last_error().decode()}")
+    return int(out[0]), int(out[1])
+
+
 def unc_reasons(status: np.ndarray) -> dict:
     """Counts of each certification reason in status words returned with set_resolve(False)."""
     st = np.asarray(status, dtype=np.int64)

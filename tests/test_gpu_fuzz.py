@@ -148,6 +148,56 @@ def test_large_default_degenerate_after_pending_sweep(gpu):
         assert ex.max() <= TOL and ef.max() <= TOL
 
 
+def _bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view(np.int64) if a.dtype == np.float64 else a
+
+
+def _shadow_ab(pr):
+    """The n > 64 default path with the EXACT re-solve off (so every certification mark shows),
+    once with the l1 scans filtered through the fp32 copy of CI and once fp64-only; returns both
+    results and the shadow path's (scans tried, scans settled)."""
+    import qpgpu
+
+    qpgpu.set_resolve(False)
+    try:
+        qpgpu.shadow_stats(reset=True)
+        on = qpgpu.solve_batched_host(pr)
+        stats = qpgpu.shadow_stats(reset=True)
+        qpgpu.set_shadow(False)
+        off = qpgpu.solve_batched_host(pr)
+    finally:
+        qpgpu.set_shadow(True)
+        qpgpu.set_resolve(True)
+    return on, off, stats
+
+
+@pytest.mark.parametrize("seed", range(0, 64, 2))
+def test_large_default_shadow_scan_bitwise(gpu, seed):
+    """the l1 scan from the fp32 copy of CI is a filter whose bounds only decide
+    which s_i need their fp64 sums — the same products in the same order as the fp64 scan.  On the
+    full large fuzz generator (scales to 1e+-40, where fp32 underflows or overflows and the bounds
+    must send the scan back to fp64) x, f, the status words with their certification marks and
+    the l1 passes are identical bit for bit with and without it."""
+    pr, modes = qp_cases.fuzz_case(seed, large=True)
+    on, off, (tried, settled) = _shadow_ab(pr)
+    for name, a, b in zip(("x", "f", "status", "passes"), on, off):
+        assert np.array_equal(_bits(a), _bits(b)), f"seed {seed} {modes}: {name} differs with the fp32 scan"
+    assert settled <= tried
+
+
+def test_c5_shadow_scan_bitwise_and_used(gpu):
+    """C5's shape (n = 256, p = 0, m = 512; the bench generator's first 64 QPs): bit-identical
+    results with and without the fp32 scan, which settles most of the scans there."""
+    import qpgpu
+
+    pr = qpgpu.make_problems("general", 256, 0, 512, 0, 64, seed=2026)
+    on, off, (tried, settled) = _shadow_ab(pr)
+    for name, a, b in zip(("x", "f", "status", "passes"), on, off):
+        assert np.array_equal(_bits(a), _bits(b)), f"C5: {name} differs with the fp32 scan"
+    assert tried > 0 and settled >= 0.5 * tried, (tried, settled)
+
+
 @pytest.mark.parametrize("seed", range(0, 48, 3))
 def test_fuzz_single_calls(gpu, seed):
     """The reference's own call pattern — one solve_quadprog() per QP — through the Python mirror
