@@ -321,6 +321,14 @@ __device__ __forceinline__ double colsum16(double (&v)[16]) {
 // diagnostic stamps only: slots 5..7 hold, instead of the equality-phase parts, the loop's
 // update_r cycles, step count and sum of iq over steps (1), or add_constraint's |h| chain +
 // coefficients, J sweep and R column + test cycles, equality phase and loop together (2)
+// largest block LDS (bytes) for which the S < 64 variants launch their four-waves-per-SIMD
+// instantiation (128 VGPRs); A/B builds lower it to send such shapes to the OCC 2 / 1 ones
+#ifndef QPGPU_WAVE_OCC4_LDS
+#define QPGPU_WAVE_OCC4_LDS 20480
+#endif
+#ifndef QPGPU_WAVE_OCC_SMALL  // the waves per SIMD that instantiation is compiled for
+#define QPGPU_WAVE_OCC_SMALL 4
+#endif
 #ifndef QPGPU_WAVE_GJR_CAP
 #define QPGPU_WAVE_GJR_CAP 0
 #endif
@@ -2534,8 +2542,8 @@ static hipError_t launch_wave(const QpArgs& a, hipStream_t stream, double* ws) {
   // keeps the unconstrained allocation (21.0 vs 22.0 ms).  The register-setup instantiations
   // (OCC 2 for S = 16, OCC 1) use the packed-R layout when QPGPU_WAVE_RPACK is on.
   if constexpr (S < 64 && !GJR) {
-    if (lds_bytes <= 20480) {
-      hipLaunchKernelGGL((QP_WAVE_KERNEL<S, NMAX, MMAX, GJR, 4>), dim3((unsigned)blocks), dim3(C::BS),
+    if (lds_bytes <= QPGPU_WAVE_OCC4_LDS) {
+      hipLaunchKernelGGL((QP_WAVE_KERNEL<S, NMAX, MMAX, GJR, QPGPU_WAVE_OCC_SMALL>), dim3((unsigned)blocks), dim3(C::BS),
                          lds_bytes, stream, a, ws);
       return hipGetLastError();
     }
