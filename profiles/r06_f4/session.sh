@@ -1,0 +1,16 @@
+# the final tree (round 6, after the fp32-copy scan): GPU suite, smoke, C1-C3 bench lines, rocprof trace of C1, HBM counters
+O=gpurun_out/r06_f4
+mkdir -p $O
+export TMPDIR=/tmp
+step() { local name=$1 lim=$2; shift 2; echo "[$(date +%T)] $name"; timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -2 $O/$name.log | cut -c1-300; if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then echo STOP; exit $rc; fi; }
+step pytest 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python -u bench.py
+step prof_C1 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_C1 -o k -- python3 bench.py --no-cpu --no-c4
+step pmcf_C1 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmcf_C1 -o k -- python3 bench.py --config C1 --steps 5 --warmup 1 --no-cpu --no-c4 --streams 1 --kernel-reps 5 --kernel-rounds 1 --prewarm-ms 0
+step pmcw_C1 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmcw_C1 -o k -- python3 bench.py --config C1 --steps 5 --warmup 1 --no-cpu --no-c4 --streams 1 --kernel-reps 5 --kernel-rounds 1 --prewarm-ms 0
+for c in C2 mgqp C3; do
+  step bench_$c 600 python -u bench.py --config $c
+  step pmcf_$c 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmcf_$c -o k -- python3 bench.py --config $c --steps 5 --warmup 1 --no-cpu --no-c4 --streams 1 --kernel-reps 5 --kernel-rounds 1 --prewarm-ms 0
+  step pmcw_$c 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmcw_$c -o k -- python3 bench.py --config $c --steps 5 --warmup 1 --no-cpu --no-c4 --streams 1 --kernel-reps 5 --kernel-rounds 1 --prewarm-ms 0
+done
