@@ -655,9 +655,10 @@ def main():
             qpgpu.shadow_stats(reset=True)
             hb.launcher(cs)()
             torch.cuda.synchronize(dev)
-            tried, settled = qpgpu.shadow_stats(reset=True)
+            tried, settled, reev = qpgpu.shadow_stats(reset=True)
             cert = {"qps": B, "marked_for_exact_resolve": qpgpu.unc_reasons(hb.status[:B].cpu().numpy()),
                     "l1_scans": {"from_fp32_copy_tried": tried, "settled_by_its_bounds": settled,
+                                 "fp64_candidate_sums": reev,
                                  "note": "DESIGN §6.7: the other scans (and every scan with --no-shadow) "
                                          "read CI in fp64"},
                     "note": "QPs the tolerance mode cannot certify (a near-dependent add, a decision "

@@ -345,7 +345,7 @@ __device__ __forceinline__ double colsum16(double (&v)[16]) {
 constexpr int kShadowCand = 16;  // most exact re-evaluations per shadow scan (else the fp64 scan)
 // diagnostic counts (qpgpu_debug_shadow_stats): l1 scans that tried the fp32 copy, and those the
 // bounds settled (one atomic per QP and scan, by the lead)
-__device__ unsigned long long g_shadow_stats[2];
+__device__ unsigned long long g_shadow_stats[3];  // [2]: fp64 re-evaluations (candidates)
 #ifndef QPGPU_WAVE_SHADOW_U  // fp32 CI loads per constraint and chunk of the shadow scan
 #define QPGPU_WAVE_SHADOW_U 32
 #endif
@@ -1965,6 +1965,7 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
     grp_sync<S>();
     const int cnt = cl[0];
     if (cnt > kShadowCand) return false;
+    if (lead) atomicAdd(&g_shadow_stats[2], (unsigned long long)cnt);
     for (int c = 0; c < cnt; c++) {
       const int i = cl[1 + c];
       if (ls < n) P[ls] = EL(CIb, ls * m + i) * xv[ls];
@@ -2718,12 +2719,13 @@ extern "C" void qpk_set_resolve(int on) { g_resolve = on != 0; }
 // test / diagnostic hook (qpgpu_debug_set_shadow): 0 scans in fp64 only
 extern "C" void qpk_set_shadow(int on) { g_shadow = on != 0 && QPGPU_WAVE_SHADOW != 0; }
 // diagnostic (qpgpu_debug_shadow_stats): out[0] scans that tried the fp32 copy, out[1] those it
-// settled, since the last reset; device-synchronous
+// settled, out[2] the fp64 re-evaluations of candidates they made, since the last reset;
+// device-synchronous
 extern "C" hipError_t qpk_shadow_stats(unsigned long long* out, int reset) {
   hipError_t e = hipDeviceSynchronize();
-  if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(qpk::g_shadow_stats), 2 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(qpk::g_shadow_stats), 3 * sizeof(unsigned long long));
   if (e == hipSuccess && reset) {
-    const unsigned long long z[2] = {0, 0};
+    const unsigned long long z[3] = {0, 0, 0};
     e = hipMemcpyToSymbol(HIP_SYMBOL(qpk::g_shadow_stats), z, sizeof(z));
   }
   return e;

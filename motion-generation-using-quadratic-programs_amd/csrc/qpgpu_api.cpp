@@ -686,15 +686,15 @@ void qpgpu_debug_set_resolve(int on) { qpk_set_resolve(on); }
 extern "C" void qpk_set_shadow(int on);
 void qpgpu_debug_set_shadow(int on) { qpk_set_shadow(on); }
 // Diagnostic (not in include/qpgpu.h): out[0] = l1 scans of the n > 64 default path that tried
-// the fp32 copy of CI, out[1] = those its bounds settled, since the last reset (reset != 0
-// zeroes them after reading).  Synchronises the current device.
+// the fp32 copy of CI, out[1] = those its bounds settled, out[2] = the fp64 re-evaluations of
+// candidates those made, since the last reset (reset != 0 zeroes them after reading).
+// Synchronises the current device.
 extern "C" hipError_t qpk_shadow_stats(unsigned long long* out, int reset);
 int qpgpu_debug_shadow_stats(uint64_t* out, int reset) {
-  unsigned long long v[2] = {0, 0};
+  unsigned long long v[3] = {0, 0, 0};
   const hipError_t e = qpk_shadow_stats(v, reset);
   if (e != hipSuccess) return hip_fail(e, "shadow stats");
-  out[0] = v[0];
-  out[1] = v[1];
+  for (int k = 0; k < 3; k++) out[k] = v[k];
   return QPGPU_SUCCESS;
 }
 

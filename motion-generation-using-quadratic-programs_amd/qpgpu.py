@@ -178,16 +178,16 @@ def set_shadow(on: bool) -> None:
 
 
 def shadow_stats(reset: bool = True) -> tuple:
-    """(l1 scans of the n > 64 default path that tried the fp32 copy of CI, scans it settled)
-    since the last reset; synchronises the device."""
+    """(l1 scans of the n > 64 default path that tried the fp32 copy of CI, scans it settled, fp64
+    re-evaluations of candidates in those) since the last reset; synchronises the device."""
     fn = LIB.qpgpu_debug_shadow_stats
     fn.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     fn.restype = ctypes.c_int
-    out = (ctypes.c_uint64 * 2)()
+    out = (ctypes.c_uint64 * 3)()
     rc = fn(out, 1 if reset else 0)
     if rc:
         raise QpgpuError(f"qpgpu_debug_shadow_stats: {rc} {LIB.qpgpu_last_error().decode()}")
-    return int(out[0]), int(out[1])
+    return int(out[0]), int(out[1]), int(out[2])
 
 
 def unc_reasons(status: np.ndarray) -> dict:

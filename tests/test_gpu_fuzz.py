@@ -163,7 +163,7 @@ def _shadow_ab(pr):
     try:
         qpgpu.shadow_stats(reset=True)
         on = qpgpu.solve_batched_host(pr)
-        stats = qpgpu.shadow_stats(reset=True)
+        stats = qpgpu.shadow_stats(reset=True)[:2]
         qpgpu.set_shadow(False)
         off = qpgpu.solve_batched_host(pr)
     finally:
