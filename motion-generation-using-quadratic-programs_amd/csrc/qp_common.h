@@ -345,9 +345,6 @@ constexpr uint32_t kArgAligned16 = 0x80000000u;
 // internal QpArgs.flags bit: the workspace already holds the setup (qp_panel.hip) — J, x0, f0,
 // c1, c2 and the Cholesky status — so the loop kernel starts at the equality phase
 constexpr uint32_t kSetupDone = 0x40000000u;
-// internal QpArgs.flags bit: outputs in mapped host memory polled by the host (the host entry's
-// zero-copy path): the lane kernel stores x, f, iters, then a system-scope fence, then status
-constexpr uint32_t kArgHostPoll = 0x10000000u;
 // internal QpArgs.flags bit: the EXACT re-solve launch after a tolerance-mode launch — only the
 // QPs whose status carries kStResolve are solved (one QP per workgroup: the others exit at once)
 constexpr uint32_t kResolveOnly = 0x20000000u;

@@ -1241,9 +1241,6 @@ __device__ __forceinline__ bool lane_body(const QpArgs& a, double* sbuf) {
     }
     a.f[b] = fval;
     if (a.iters) a.iters[b] = iter;
-    // zero-copy host entry: the host polls the status word, so x, f and iters must be visible
-    // in host memory before it (qpk::kArgHostPoll; a uniform branch, off in batched launches)
-    if (a.flags & kArgHostPoll) __threadfence_system();
     a.status[b] = status;
   }
   lstamp(a, 4);

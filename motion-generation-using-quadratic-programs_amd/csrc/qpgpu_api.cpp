@@ -351,12 +351,6 @@ static bool family_covers(uint32_t flags, int n, int p, int m) {
   return qpgpu_kernel_name(n, p, m)[0] != 0;
 }
 
-// Does the launch for these flags run the lane kernel (whose zero-copy stores end with the status
-// word behind a system-scope fence)?
-static bool family_poll(uint32_t flags, int n, int p, int m) {
-  if (flags & (QPGPU_FLAG_FORCE_SUBGROUP | QPGPU_FLAG_FORCE_WAVE | QPGPU_FLAG_FORCE_GENERIC)) return false;
-  return qpk_lane_name(n, p, m) != nullptr;
-}
 
 // Host-pointer entry (the drop-in's path, one QP per solve_quadprog() call, and the batched
 // controller's).  Device buffers are one allocation per thread, laid out
@@ -371,10 +365,8 @@ static bool family_poll(uint32_t flags, int n, int p, int m) {
 static constexpr size_t kStagedBytes = 4u << 20;
 // Batches up to g_zero_copy_bytes (a few dozen C1 QPs; one drop-in solve_quadprog() call is 2 KB)
 // skip both copies: the kernel reads its inputs from, and writes its outputs to, the pinned
-// staging buffer itself (mapped host memory), and the call synchronises the stream once.
-// With the status-word poll below, one C1 call is 34.5 us host to host (41.3 with the copies;
-// profiles/r06_s11/latency_parts.log) and one drop-in solve_quadprog() 34.7 us p50 (39.9 in round
-// 5).  Measured per shape before the poll, host to host with the factor written
+// staging buffer itself (mapped host memory), and the call waits for the stream's completion
+// once (a hipStreamQuery spin).  Measured per shape, host to host with the factor written
 // back as the drop-in asks (profiles/r06_s6/latency_parts.log, copies -> zero-copy): (7, 6, 14)
 // 42.6 -> 38.6 us, (14, 10, 28) 85.3 -> 82.0, (30, 6, 60) 214.1 -> 208.2, but (8, 0, 16)
 // 61.2 -> 65.1: without an equality phase the first l1 scan waits on the host-memory reads of CI
@@ -473,32 +465,23 @@ int qpgpu_solve_batched_host(const qpgpu_problem_desc* d, double* G, const doubl
     if (total <= g_zero_copy_bytes && d->p > 0) {
       // zero-copy: the kernel works on the mapped staging buffer directly
       auto Hp = [&](size_t off) { return reinterpret_cast<double*>(h + off); };
-      // The lane kernel (n <= 8, m <= 16) stores x, f and iters, then a system-scope fence,
-      // then the status word (qpk::kArgHostPoll): the host spins on the status words it
-      // poisoned instead of waiting for the stream's completion signal (~5 us of a single call).
-      // Other kernels, and a kernel that ends without writing them, take the stream sync.
-      const bool poll = family_poll(d->flags, d->n, d->p, d->m);
-      volatile int32_t* const hst = reinterpret_cast<volatile int32_t*>(h + os);
       rc = solve_batched_impl(d, Hp(oG), Hp(og0), Hp(oCE), Hp(oce0), Hp(oCI), Hp(oci0), Hp(ox), Hp(of),
                               reinterpret_cast<int32_t*>(h + os), reinterpret_cast<int32_t*>(h + oi),
-                              nullptr, nullptr, nullptr, s, poll ? qpk::kArgHostPoll : 0u);
+                              nullptr, nullptr, nullptr, s);
       if (rc) {
         (void)hipStreamSynchronize(s);
         return rc;
       }
-      bool done = false;
-      if (poll) {
-        for (long spin = 0; !done; ++spin) {
-          done = true;
-          for (size_t b = 0; b < B && done; b++) done = hst[b] != -1;
-          if (!done && (spin & 4095) == 4095) {
-            e = hipStreamQuery(s);  // finished without writing, or failed: leave to the sync below
-            if (e != hipErrorNotReady) break;
-          }
-        }
-        std::atomic_thread_fence(std::memory_order_acquire);
+      // The outputs are read once the stream reports the kernel complete (its end-of-kernel
+      // release makes every store visible), by spinning on hipStreamQuery rather than blocking in
+      // hipStreamSynchronize.  Polling the status words instead (the kernel storing x, f, iters, a
+      // system-scope fence, then the status; round 6's first form) raced: a status word was seen
+      // with x, or the factor's last rows, still the values the host had staged — in the
+      // coarse-grained pinned buffer and in a fine-grained one alike (tests/test_gpu_dropin.py::
+      // test_eigen_api_matches_oracle, test_single_calls_outputs_fresh; profiles/r06_f6, r06_s26).
+      while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
       }
-      if (!done && (e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+      if (e != hipSuccess) return hip_fail(e, "hipStreamQuery");
       std::memcpy(x, h + ox, nx);
       std::memcpy(f, h + of, nf);
       std::memcpy(status, h + os, ns);

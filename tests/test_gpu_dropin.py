@@ -112,3 +112,28 @@ def test_eigen_api_matches_oracle(gpu, tmp_path, kind, n, p, m):
             assert np.float64(float.fromhex(tok[2])).view(np.uint64) == np.float64(f).view(np.uint64)
             xs = np.array([float.fromhex(t) for t in tok[3:]])
             assert np.array_equal(xs.view(np.uint64), x.view(np.uint64)), (q, tok[0])
+
+
+def test_single_calls_outputs_fresh(gpu):
+    """The zero-copy host entry (the drop-in's path) once returned the previous call's x with the
+    new call's status and f (profiles/r06_f6: the outputs then shared the coarse-grained staging
+    buffer, whose L2 write-backs the status word could overtake).  3 000 consecutive single
+    (7, 6, 14) solves of distinct QPs through the host entry: x, f, status and the factor written
+    back bitwise against the oracle every time (a stale x would be the zeros passed in)."""
+    import numpy as np
+
+    import oracle
+    import qpgpu
+
+    n, p, m, B = 7, 6, 14, 3000
+    pr = qpgpu.make_problems("general", n, p, m, 0, B, seed=77)
+    prc = qpgpu.Problems(n, p, m, pr.G.copy(), pr.g0, pr.CE, pr.ce0, pr.CI, pr.ci0)
+    xo, fo, so, _ = oracle.solve_batch(prc, write_factor=True, max_steps=1000 + 100 * (n + p + m))
+    for q in range(B):
+        one = qpgpu.Problems(n, p, m, pr.G[q:q + 1].copy(), pr.g0[q:q + 1], pr.CE[q:q + 1], pr.ce0[q:q + 1],
+                             pr.CI[q:q + 1], pr.ci0[q:q + 1])
+        x, f, st, _ = qpgpu.solve_batched_host(one, write_factor=True)
+        assert st[0] == so[q], q
+        assert np.float64(f[0]).view(np.uint64) == np.float64(fo[q]).view(np.uint64), q
+        assert np.array_equal(x[0].view(np.uint64), xo[q].view(np.uint64)), (q, x[0], xo[q])
+        assert np.array_equal(one.G.view(np.uint64), prc.G[q:q + 1].view(np.uint64)), q
