@@ -329,6 +329,11 @@ __device__ __forceinline__ double colsum16(double (&v)[16]) {
 #ifndef QPGPU_WAVE_OCC_SMALL  // the waves per SIMD that instantiation is compiled for
 #define QPGPU_WAVE_OCC_SMALL 4
 #endif
+// waves per SIMD the workspace variant's registers are allocated for (4: 128 VGPRs, four resident
+// QPs per CU; an A/B build may lower it)
+#ifndef QPGPU_WAVE_GJR_OCC
+#define QPGPU_WAVE_GJR_OCC 4
+#endif
 #ifndef QPGPU_WAVE_GJR_CAP
 #define QPGPU_WAVE_GJR_CAP 0
 #endif
@@ -2510,7 +2515,7 @@ __device__ __forceinline__ bool wave_body(const QpArgs& a, double* __restrict__ 
 }
 
 template <int S, int NMAX, int MMAX, bool GJR, int OCC = 1>
-__global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? 4 : OCC)
+__global__ void __launch_bounds__(S >= 64 ? S : 64, GJR ? QPGPU_WAVE_GJR_OCC : OCC)
     QP_WAVE_KERNEL(const QpArgs a, double* __restrict__ ws) {
   if constexpr (GJR) {
     // the EXACT re-solve after a tolerance-mode launch: only the QPs marked for it (one QP per
